@@ -1,0 +1,46 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+if GOLDEN not in sys.path:
+    sys.path.insert(0, GOLDEN)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+
+
+def load_golden(name):
+    """Fixture dict (+ regenerated X when it is not stored)."""
+    import make_golden  # tests/golden/make_golden.py (no reference import at module load)
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    out = {key: z[key] for key in z.files}
+    if "X" in out:
+        X = out["X"].astype(np.float64)
+    else:
+        X = make_golden.case_data(make_golden.CASES[name]["data"])
+    assert make_golden.x_digest(X) == str(out["x_sha256"]), f"{name}: regenerated data drifted"
+    out["X"] = X
+    out["stdout"] = str(out["stdout"])
+    return out
+
+
+GOLDEN_CASES = ["test_a", "test_c", "test_d", "test_e_p3", "test_b_small", "empty", "ties",
+                "c2_small", "c3_small", "c4_small"]
+
+
+@pytest.fixture(scope="session")
+def golden():
+    cache = {}
+
+    def get(name):
+        if name not in cache:
+            cache[name] = load_golden(name)
+        return cache[name]
+    return get
