@@ -1,0 +1,67 @@
+// Internal declarations shared by km_kernels.hip (device code + launchers)
+// and km_runtime.hip (context, memory, C-ABI).  Not part of the public ABI
+// (that is include/kmeans_amd.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace km {
+
+// Ambiguous-point queue entry written by the screening kernels and consumed
+// by k_resolve (exact float64 re-rank of the reference's np.argmin).
+struct QEntry {
+  uint32_t row;   // local row
+  uint32_t i1;    // best screened centroid
+  uint32_t i2;    // second best screened centroid
+  uint32_t kind;  // 1 = re-rank {i1,i2}, 2 = full exact scan
+};
+
+// Per-iteration status produced on device by k_finalize (kmeans_spark.py:176-313
+// quantities), copied to pinned host memory by km_update.
+struct DevStatus {
+  double sse;          // SSE of the assignment w.r.t. the pre-update centroids (L224-237)
+  double max_shift;    // max_c ||new_c - old_c||  (L293-294), empties kept at old
+  int32_t n_empty;     // clusters with no points (L186-188)
+  int32_t nonfinite;   // any non-finite new centroid (L289)
+  int32_t q_rerank;    // screened points re-ranked exactly
+  int32_t q_full;      // screened points that needed the full exact scan
+};
+
+struct Geometry {
+  int64_t n;    // local rows
+  int32_t d;    // features
+  int32_t dp;   // padded row stride of X (floats), multiple of 16
+  int32_t k;    // clusters
+  int32_t kp;   // padded cluster count (multiple of 32)
+};
+
+// ---- launchers (km_kernels.hip) -------------------------------------------
+hipError_t launch_prep_centroids(const double* C64, const Geometry& g, float* C32, __bf16* Chi,
+                                 __bf16* Clo, float* cn2, float* cmax, hipStream_t s);
+// Small k*d path: direct-form fp32 screening, in-thread exact re-rank,
+// optional fused statistics (LDS float64 table, replicated per lane).
+hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C32, const double* C64,
+                               const float* cmax, int32_t* labels, double* stats, int fuse_stats,
+                               int n_cu, hipStream_t s);
+bool small_path_ok(const Geometry& g);
+// MFMA path: bf16x3 screening on v_mfma_f32_32x32x16_bf16, top-3 keys,
+// ambiguous points queued for k_resolve.
+hipError_t launch_assign_mfma(const float* X, const Geometry& g, const __bf16* Chi, const __bf16* Clo,
+                              const float* cn2, const float* cmax, int32_t* labels, QEntry* queue,
+                              uint32_t* qcount, int n_cu, hipStream_t s);
+bool mfma_path_ok(const Geometry& g);
+hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const QEntry* queue,
+                          const uint32_t* qcount, int32_t* labels, int n_cu, hipStream_t s);
+hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels, double* stats, int n_cu,
+                        hipStream_t s);
+hipError_t launch_update(const double* stats, const double* C64_old, const double* mu, const Geometry& g,
+                         double* C64_new, double* work, int64_t* counts, const double* sse_base,
+                         const uint32_t* qcount, DevStatus* status, hipStream_t s);
+hipError_t launch_sum_x(const float* X, const Geometry& g, double* out, hipStream_t s);
+hipError_t launch_sq_dev(const float* X, const Geometry& g, const double* mu, double* out, hipStream_t s);
+hipError_t launch_gather_rows(const float* X, const Geometry& g, const int64_t* idx, int32_t n, double* out,
+                              hipStream_t s);
+hipError_t launch_gen_blobs(float* X, const Geometry& g, int64_t row_offset, int32_t n_centers, float box,
+                            float stddev, uint64_t seed, hipStream_t s);
+
+}  // namespace km

@@ -1,0 +1,572 @@
+// Context, device memory, streams and the C-ABI of include/kmeans_amd.h.
+//
+// One km_ctx per GPU (one process per GPU, torch.distributed ranks).  All
+// per-iteration work is enqueued on ctx->stream; only calls that hand host
+// data back synchronise it.  See DESIGN.md for the data layout in HBM.
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/kmeans_amd.h"
+#include "km_internal.h"
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define KM_HIP(call)                                                                               \
+  do {                                                                                             \
+    hipError_t e_ = (call);                                                                        \
+    if (e_ != hipSuccess)                                                                          \
+      return fail(KM_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_) + " (" +           \
+                                  std::to_string((int)e_) + ")");                                  \
+  } while (0)
+
+#define KM_REQUIRE(cond, code, msg) \
+  do {                              \
+    if (!(cond)) return fail(code, msg); \
+  } while (0)
+
+template <class T>
+void dfree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+template <class T>
+void hfree(T*& p) {
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+}
+
+constexpr int kAllowedDp[] = {16, 32, 48, 64, 96, 128, 192, 256};
+
+int choose_dp(int d) {
+  for (int v : kAllowedDp)
+    if (d <= v) return v;
+  return (d + 15) / 16 * 16;  // unsupported by the screening kernels (reported at assign time)
+}
+}  // namespace
+
+struct km_ctx {
+  int device = 0;
+  int n_cu = 256;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  km::Geometry g{};
+  bool loaded = false;
+  bool have_c = false;
+  int path = 0;  // 1 small, 2 mfma
+  // data
+  float* X = nullptr;
+  int32_t* labels = nullptr;
+  km::QEntry* queue = nullptr;
+  uint32_t* qcount = nullptr;
+  double* moments = nullptr;  // d+1 scratch
+  double* mu = nullptr;       // d
+  double* sse_base = nullptr; // 1
+  int64_t* idx_scratch = nullptr;
+  double* rows_scratch = nullptr;
+  int64_t scratch_rows = 0;
+  // centroids
+  int k_alloc = 0;
+  double* C64_cur = nullptr;
+  double* C64_new = nullptr;
+  float* C32 = nullptr;
+  __bf16* Chi = nullptr;
+  __bf16* Clo = nullptr;
+  float* cn2 = nullptr;
+  float* cmax = nullptr;
+  double* stats_own = nullptr;
+  double* stats = nullptr;
+  double* work = nullptr;
+  int64_t* counts_dev = nullptr;
+  km::DevStatus* status_dev = nullptr;
+  km::DevStatus* status_host = nullptr;
+  int64_t* counts_host = nullptr;
+  // staging
+  float* pinned = nullptr;
+  size_t pinned_floats = 0;
+  // profiling
+  bool prof = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[KM_K_COUNT];
+  std::vector<hipEvent_t> pool;
+
+  hipEvent_t take_event() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+};
+
+namespace {
+
+struct ProfScope {
+  km_ctx* c;
+  int kind;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(km_ctx* ctx, int k) : c(ctx), kind(k) {
+    if (c->prof) {
+      a = c->take_event();
+      b = c->take_event();
+      (void)hipEventRecord(a, c->stream);
+    }
+  }
+  ~ProfScope() {
+    if (c->prof) {
+      (void)hipEventRecord(b, c->stream);
+      c->ev[kind].emplace_back(a, b);
+    }
+  }
+};
+
+void free_centroids(km_ctx* c) {
+  dfree(c->C64_cur);
+  dfree(c->C64_new);
+  dfree(c->C32);
+  dfree(c->Chi);
+  dfree(c->Clo);
+  dfree(c->cn2);
+  dfree(c->cmax);
+  dfree(c->stats_own);
+  dfree(c->work);
+  dfree(c->counts_dev);
+  dfree(c->status_dev);
+  hfree(c->status_host);
+  hfree(c->counts_host);
+  if (c->stats != nullptr && c->stats != c->stats_own) {
+    // external buffer: keep binding only if the size is unchanged (caller re-binds otherwise)
+  }
+  c->stats = nullptr;
+  c->k_alloc = 0;
+  c->have_c = false;
+}
+
+void free_data(km_ctx* c) {
+  dfree(c->X);
+  dfree(c->labels);
+  dfree(c->queue);
+  dfree(c->qcount);
+  dfree(c->moments);
+  dfree(c->mu);
+  dfree(c->sse_base);
+  dfree(c->idx_scratch);
+  dfree(c->rows_scratch);
+  c->scratch_rows = 0;
+  c->loaded = false;
+}
+
+int prep(km_ctx* c) {
+  ProfScope ps(c, KM_K_PREP);
+  KM_HIP(km::launch_prep_centroids(c->C64_cur, c->g, c->C32, c->Chi, c->Clo, c->cn2, c->cmax, c->stream));
+  return KM_OK;
+}
+
+int ensure_scratch(km_ctx* c, int64_t rows) {
+  if (rows <= c->scratch_rows) return KM_OK;
+  dfree(c->idx_scratch);
+  dfree(c->rows_scratch);
+  KM_HIP(hipMalloc(&c->idx_scratch, sizeof(int64_t) * rows));
+  KM_HIP(hipMalloc(&c->rows_scratch, sizeof(double) * rows * std::max(1, c->g.d)));
+  c->scratch_rows = rows;
+  return KM_OK;
+}
+
+int run_assign(km_ctx* c, bool with_stats) {
+  const km::Geometry& g = c->g;
+  KM_HIP(hipMemsetAsync(c->qcount, 0, 4 * sizeof(uint32_t), c->stream));
+  if (with_stats) KM_HIP(hipMemsetAsync(c->stats, 0, sizeof(double) * (size_t)g.k * (g.d + 1), c->stream));
+  if (c->path == 1) {
+    ProfScope ps(c, KM_K_ASSIGN);
+    KM_HIP(km::launch_assign_small(c->X, g, c->C32, c->C64_cur, c->cmax, c->labels, c->stats, with_stats ? 1 : 0,
+                                   c->n_cu, c->stream));
+    return KM_OK;
+  }
+  {
+    ProfScope ps(c, KM_K_ASSIGN);
+    KM_HIP(km::launch_assign_mfma(c->X, g, c->Chi, c->Clo, c->cn2, c->cmax, c->labels, c->queue, c->qcount, c->n_cu,
+                                  c->stream));
+  }
+  {
+    ProfScope ps(c, KM_K_RESOLVE);
+    KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->queue, c->qcount, c->labels, c->n_cu, c->stream));
+  }
+  if (with_stats) {
+    ProfScope ps(c, KM_K_STATS);
+    KM_HIP(km::launch_stats(c->X, g, c->labels, c->stats, c->n_cu, c->stream));
+  }
+  return KM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int km_abi_version(void) { return KM_ABI_VERSION; }
+
+const char* km_last_error(void) { return g_err.c_str(); }
+
+int km_device_count(int* out) {
+  KM_REQUIRE(out, KM_ERR_ARG, "km_device_count: null out");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *out = n;
+  return KM_OK;
+}
+
+int km_create(int device, km_ctx** out) {
+  KM_REQUIRE(out, KM_ERR_ARG, "km_create: null out");
+  *out = nullptr;
+  int n = 0;
+  KM_HIP(hipGetDeviceCount(&n));
+  KM_REQUIRE(device >= 0 && device < n, KM_ERR_ARG,
+             "km_create: device " + std::to_string(device) + " out of range (" + std::to_string(n) + " devices)");
+  KM_HIP(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  KM_HIP(hipGetDeviceProperties(&prop, device));
+  KM_REQUIRE(std::string(prop.gcnArchName).rfind("gfx950", 0) == 0, KM_ERR_UNSUPPORTED,
+             std::string("km_create: kernels are built for gfx950 (MI355X), device is ") + prop.gcnArchName);
+  km_ctx* c = new km_ctx();
+  c->device = device;
+  c->n_cu = prop.multiProcessorCount;
+  hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(KM_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return KM_OK;
+}
+
+int km_destroy(km_ctx* c) {
+  if (!c) return KM_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  free_centroids(c);
+  free_data(c);
+  hfree(c->pinned);
+  for (auto& v : c->ev)
+    for (auto& p : v) {
+      (void)hipEventDestroy(p.first);
+      (void)hipEventDestroy(p.second);
+    }
+  for (auto e : c->pool) (void)hipEventDestroy(e);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+  return KM_OK;
+}
+
+int km_set_stream(km_ctx* c, void* s) {
+  KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
+  KM_HIP(hipSetDevice(c->device));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
+  return KM_OK;
+}
+
+int km_sync(km_ctx* c) {
+  KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
+  KM_HIP(hipSetDevice(c->device));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  return KM_OK;
+}
+
+int km_info_get(km_ctx* c, km_info* out) {
+  KM_REQUIRE(c && out, KM_ERR_ARG, "null arg");
+  out->n = c->g.n;
+  out->d = c->g.d;
+  out->dp = c->g.dp;
+  out->k = c->g.k;
+  out->kp = c->g.kp;
+  out->path = c->path;
+  out->n_cu = c->n_cu;
+  out->device = c->device;
+  out->fused_stats = (c->path == 1);
+  return KM_OK;
+}
+
+int km_load_begin(km_ctx* c, int64_t n, int32_t d) {
+  KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
+  KM_REQUIRE(n >= 0 && n < (int64_t)UINT32_MAX, KM_ERR_ARG, "km_load_begin: n out of range");
+  KM_REQUIRE(d > 0, KM_ERR_ARG, "km_load_begin: d must be positive");
+  KM_HIP(hipSetDevice(c->device));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  free_data(c);
+  free_centroids(c);
+  c->g = km::Geometry{};
+  c->g.n = n;
+  c->g.d = d;
+  c->g.dp = choose_dp(d);
+  const int64_t rows = std::max<int64_t>(n, 1);
+  KM_HIP(hipMalloc(&c->X, sizeof(float) * rows * c->g.dp));
+  KM_HIP(hipMemsetAsync(c->X, 0, sizeof(float) * rows * c->g.dp, c->stream));
+  KM_HIP(hipMalloc(&c->labels, sizeof(int32_t) * rows));
+  KM_HIP(hipMalloc(&c->queue, sizeof(km::QEntry) * rows));
+  KM_HIP(hipMalloc(&c->qcount, 4 * sizeof(uint32_t)));
+  KM_HIP(hipMalloc(&c->moments, sizeof(double) * (d + 1)));
+  KM_HIP(hipMalloc(&c->mu, sizeof(double) * d));
+  KM_HIP(hipMemsetAsync(c->mu, 0, sizeof(double) * d, c->stream));
+  KM_HIP(hipMalloc(&c->sse_base, sizeof(double)));
+  KM_HIP(hipMemsetAsync(c->sse_base, 0, sizeof(double), c->stream));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  c->loaded = true;
+  return KM_OK;
+}
+
+int km_load_rows(km_ctx* c, int64_t row0, const float* rows, int64_t nrows) {
+  KM_REQUIRE(c && c->loaded, KM_ERR_STATE, "km_load_rows: call km_load_begin first");
+  KM_REQUIRE(row0 >= 0 && nrows >= 0 && row0 + nrows <= c->g.n, KM_ERR_ARG, "km_load_rows: rows out of range");
+  if (nrows == 0) return KM_OK;
+  KM_REQUIRE(rows, KM_ERR_ARG, "km_load_rows: null rows");
+  KM_HIP(hipSetDevice(c->device));
+  const int d = c->g.d, dp = c->g.dp;
+  const size_t chunk_floats = (size_t)16 << 20;  // 64 MiB pinned staging
+  if (!c->pinned) {
+    KM_HIP(hipHostMalloc(&c->pinned, chunk_floats * sizeof(float), hipHostMallocDefault));
+    c->pinned_floats = chunk_floats;
+  }
+  const int64_t per = std::max<int64_t>(1, (int64_t)(c->pinned_floats / d));
+  for (int64_t r = 0; r < nrows; r += per) {
+    const int64_t m = std::min(per, nrows - r);
+    memcpy(c->pinned, rows + r * d, sizeof(float) * m * d);
+    KM_HIP(hipMemcpy2DAsync(c->X + (row0 + r) * dp, sizeof(float) * dp, c->pinned, sizeof(float) * d,
+                            sizeof(float) * d, m, hipMemcpyHostToDevice, c->stream));
+    KM_HIP(hipStreamSynchronize(c->stream));
+  }
+  return KM_OK;
+}
+
+int km_generate_blobs(km_ctx* c, int64_t n, int32_t d, int64_t global_row0, int32_t n_centers, float box,
+                      float stddev, uint64_t seed) {
+  KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
+  KM_REQUIRE(n_centers > 0, KM_ERR_ARG, "n_centers must be positive");
+  int rc = km_load_begin(c, n, d);
+  if (rc != KM_OK) return rc;
+  KM_HIP(km::launch_gen_blobs(c->X, c->g, global_row0, n_centers, box, stddev, seed, c->stream));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  return KM_OK;
+}
+
+int km_sum_x(km_ctx* c, double* out) {
+  KM_REQUIRE(c && c->loaded && out, KM_ERR_STATE, "km_sum_x: no data");
+  KM_HIP(hipSetDevice(c->device));
+  KM_HIP(hipMemsetAsync(c->moments, 0, sizeof(double) * (c->g.d + 1), c->stream));
+  KM_HIP(km::launch_sum_x(c->X, c->g, c->moments, c->stream));
+  KM_HIP(hipMemcpyAsync(out, c->moments, sizeof(double) * c->g.d, hipMemcpyDeviceToHost, c->stream));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  return KM_OK;
+}
+
+int km_sq_dev(km_ctx* c, const double* mu, double* out_local) {
+  KM_REQUIRE(c && c->loaded && mu && out_local, KM_ERR_STATE, "km_sq_dev: no data");
+  KM_HIP(hipSetDevice(c->device));
+  KM_HIP(hipMemcpyAsync(c->mu, mu, sizeof(double) * c->g.d, hipMemcpyHostToDevice, c->stream));
+  KM_HIP(hipMemsetAsync(c->moments, 0, sizeof(double), c->stream));
+  KM_HIP(km::launch_sq_dev(c->X, c->g, c->mu, c->moments, c->stream));
+  KM_HIP(hipMemcpyAsync(out_local, c->moments, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  return KM_OK;
+}
+
+int km_set_sse_base(km_ctx* c, double v) {
+  KM_REQUIRE(c && c->loaded, KM_ERR_STATE, "km_set_sse_base: no data");
+  KM_HIP(hipSetDevice(c->device));
+  KM_HIP(hipMemcpyAsync(c->sse_base, &v, sizeof(double), hipMemcpyHostToDevice, c->stream));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  return KM_OK;
+}
+
+int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
+  KM_REQUIRE(c && c->loaded, KM_ERR_STATE, "km_set_centroids: load data first");
+  KM_REQUIRE(C, KM_ERR_ARG, "km_set_centroids: null C");
+  KM_REQUIRE(k > 0, KM_ERR_ARG, "km_set_centroids: k must be positive");
+  KM_REQUIRE(d == c->g.d, KM_ERR_ARG,
+             "km_set_centroids: d=" + std::to_string(d) + " != data d=" + std::to_string(c->g.d));
+  KM_HIP(hipSetDevice(c->device));
+  if (k != c->k_alloc) {
+    KM_HIP(hipStreamSynchronize(c->stream));
+    double* external = (c->stats && c->stats != c->stats_own) ? c->stats : nullptr;
+    (void)external;
+    free_centroids(c);
+    c->g.k = k;
+    c->g.kp = (k + 31) / 32 * 32;
+    const int kp = c->g.kp, dp = c->g.dp;
+    KM_HIP(hipMalloc(&c->C64_cur, sizeof(double) * k * d));
+    KM_HIP(hipMalloc(&c->C64_new, sizeof(double) * k * d));
+    KM_HIP(hipMalloc(&c->C32, sizeof(float) * kp * dp));
+    KM_HIP(hipMalloc(&c->Chi, sizeof(__bf16) * kp * dp));
+    KM_HIP(hipMalloc(&c->Clo, sizeof(__bf16) * kp * dp));
+    KM_HIP(hipMalloc(&c->cn2, sizeof(float) * kp));
+    KM_HIP(hipMalloc(&c->cmax, sizeof(float)));
+    KM_HIP(hipMalloc(&c->stats_own, sizeof(double) * (size_t)k * (d + 1)));
+    KM_HIP(hipMalloc(&c->work, sizeof(double) * 3 * k));
+    KM_HIP(hipMalloc(&c->counts_dev, sizeof(int64_t) * k));
+    KM_HIP(hipMalloc(&c->status_dev, sizeof(km::DevStatus)));
+    KM_HIP(hipHostMalloc(&c->status_host, sizeof(km::DevStatus), hipHostMallocDefault));
+    KM_HIP(hipHostMalloc(&c->counts_host, sizeof(int64_t) * k, hipHostMallocDefault));
+    c->stats = c->stats_own;
+    c->k_alloc = k;
+    if (km::small_path_ok(c->g))
+      c->path = 1;
+    else if (km::mfma_path_ok(c->g))
+      c->path = 2;
+    else
+      c->path = 0;
+  }
+  KM_HIP(hipMemcpyAsync(c->C64_cur, C, sizeof(double) * k * d, hipMemcpyHostToDevice, c->stream));
+  int rc = prep(c);
+  if (rc != KM_OK) return rc;
+  KM_HIP(hipStreamSynchronize(c->stream));
+  c->have_c = true;
+  return KM_OK;
+}
+
+int km_get_centroids(km_ctx* c, int32_t which, double* out) {
+  KM_REQUIRE(c && c->have_c && out, KM_ERR_STATE, "km_get_centroids: no centroids");
+  KM_HIP(hipSetDevice(c->device));
+  const double* src = which ? c->C64_new : c->C64_cur;
+  KM_HIP(hipMemcpyAsync(out, src, sizeof(double) * c->g.k * c->g.d, hipMemcpyDeviceToHost, c->stream));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  return KM_OK;
+}
+
+int km_assign_stats(km_ctx* c) {
+  KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_assign_stats: set centroids first");
+  KM_REQUIRE(c->path != 0, KM_ERR_UNSUPPORTED,
+             "km_assign_stats: no kernel for d=" + std::to_string(c->g.d) + " (supported: d <= 256)");
+  KM_HIP(hipSetDevice(c->device));
+  return run_assign(c, true);
+}
+
+int km_stats_buffer(km_ctx* c, void** p, int64_t* len) {
+  KM_REQUIRE(c && c->have_c && p && len, KM_ERR_STATE, "km_stats_buffer: set centroids first");
+  *p = c->stats;
+  *len = (int64_t)c->g.k * (c->g.d + 1);
+  return KM_OK;
+}
+
+int km_bind_stats_buffer(km_ctx* c, void* p) {
+  KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_bind_stats_buffer: set centroids first");
+  c->stats = p ? reinterpret_cast<double*>(p) : c->stats_own;
+  return KM_OK;
+}
+
+int km_update(km_ctx* c, km_status* st, int64_t* counts) {
+  KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_update: set centroids first");
+  KM_HIP(hipSetDevice(c->device));
+  {
+    ProfScope ps(c, KM_K_UPDATE);
+    KM_HIP(km::launch_update(c->stats, c->C64_cur, c->mu, c->g, c->C64_new, c->work, c->counts_dev, c->sse_base,
+                             c->qcount, c->status_dev, c->stream));
+  }
+  KM_HIP(hipMemcpyAsync(c->status_host, c->status_dev, sizeof(km::DevStatus), hipMemcpyDeviceToHost, c->stream));
+  KM_HIP(hipMemcpyAsync(c->counts_host, c->counts_dev, sizeof(int64_t) * c->g.k, hipMemcpyDeviceToHost, c->stream));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  const km::DevStatus& s = *c->status_host;
+  if (st) {
+    st->sse = s.sse;
+    st->max_shift = s.max_shift;
+    st->n_empty = s.n_empty;
+    st->nonfinite = s.nonfinite;
+    st->q_rerank = s.q_rerank;
+    st->q_full = s.q_full;
+  }
+  if (counts) memcpy(counts, c->counts_host, sizeof(int64_t) * c->g.k);
+  return s.n_empty > 0 ? KM_EMPTY : KM_OK;
+}
+
+int km_replace_rows(km_ctx* c, const int32_t* ids, const double* rows, int32_t n) {
+  KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_replace_rows: set centroids first");
+  KM_REQUIRE(n >= 0 && (n == 0 || (ids && rows)), KM_ERR_ARG, "km_replace_rows: bad args");
+  KM_HIP(hipSetDevice(c->device));
+  for (int i = 0; i < n; ++i) {
+    KM_REQUIRE(ids[i] >= 0 && ids[i] < c->g.k, KM_ERR_ARG, "km_replace_rows: cluster id out of range");
+    KM_HIP(hipMemcpyAsync(c->C64_new + (size_t)ids[i] * c->g.d, rows + (size_t)i * c->g.d,
+                          sizeof(double) * c->g.d, hipMemcpyHostToDevice, c->stream));
+  }
+  KM_HIP(hipStreamSynchronize(c->stream));
+  return KM_OK;
+}
+
+int km_commit(km_ctx* c) {
+  KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_commit: set centroids first");
+  KM_HIP(hipSetDevice(c->device));
+  std::swap(c->C64_cur, c->C64_new);
+  return prep(c);
+}
+
+int km_gather_rows(km_ctx* c, const int64_t* idx, int32_t n, double* out) {
+  KM_REQUIRE(c && c->loaded, KM_ERR_STATE, "km_gather_rows: no data");
+  if (n <= 0) return KM_OK;
+  KM_REQUIRE(idx && out, KM_ERR_ARG, "km_gather_rows: null arg");
+  for (int i = 0; i < n; ++i)
+    KM_REQUIRE(idx[i] >= 0 && idx[i] < c->g.n, KM_ERR_ARG, "km_gather_rows: index out of range");
+  KM_HIP(hipSetDevice(c->device));
+  int rc = ensure_scratch(c, n);
+  if (rc != KM_OK) return rc;
+  KM_HIP(hipMemcpyAsync(c->idx_scratch, idx, sizeof(int64_t) * n, hipMemcpyHostToDevice, c->stream));
+  KM_HIP(km::launch_gather_rows(c->X, c->g, c->idx_scratch, n, c->rows_scratch, c->stream));
+  KM_HIP(hipMemcpyAsync(out, c->rows_scratch, sizeof(double) * n * c->g.d, hipMemcpyDeviceToHost, c->stream));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  return KM_OK;
+}
+
+int km_predict(km_ctx* c, int32_t* labels_out) {
+  KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_predict: set centroids first");
+  KM_REQUIRE(c->path != 0, KM_ERR_UNSUPPORTED, "km_predict: unsupported geometry");
+  KM_HIP(hipSetDevice(c->device));
+  int rc = run_assign(c, false);
+  if (rc != KM_OK) return rc;
+  if (labels_out && c->g.n > 0)
+    KM_HIP(hipMemcpyAsync(labels_out, c->labels, sizeof(int32_t) * c->g.n, hipMemcpyDeviceToHost, c->stream));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  return KM_OK;
+}
+
+int km_labels(km_ctx* c, int32_t* labels_out) {
+  KM_REQUIRE(c && c->loaded && labels_out, KM_ERR_STATE, "km_labels: no data");
+  KM_HIP(hipSetDevice(c->device));
+  if (c->g.n > 0)
+    KM_HIP(hipMemcpyAsync(labels_out, c->labels, sizeof(int32_t) * c->g.n, hipMemcpyDeviceToHost, c->stream));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  return KM_OK;
+}
+
+int km_profile(km_ctx* c, int32_t enable) {
+  KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
+  c->prof = enable != 0;
+  return KM_OK;
+}
+
+int km_prof_read(km_ctx* c, int32_t kind, double* total_ms, int64_t* launches) {
+  KM_REQUIRE(c && kind >= 0 && kind < KM_K_COUNT, KM_ERR_ARG, "km_prof_read: bad kind");
+  KM_HIP(hipSetDevice(c->device));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  double tot = 0.0;
+  for (auto& p : c->ev[kind]) {
+    float ms = 0.0f;
+    KM_HIP(hipEventElapsedTime(&ms, p.first, p.second));
+    tot += ms;
+    c->pool.push_back(p.first);
+    c->pool.push_back(p.second);
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = (int64_t)c->ev[kind].size();
+  c->ev[kind].clear();
+  return KM_OK;
+}
+
+}  // extern "C"

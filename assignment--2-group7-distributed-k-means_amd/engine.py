@@ -1,0 +1,188 @@
+"""``HipEngine``: one GPU's share of the Lloyd iteration, driven through the
+C-ABI of ``include/kmeans_amd.h``.
+
+The engine owns one ``km_ctx`` (rows resident in HBM, centroids, statistics
+buffer, stream).  ``kmeans.LloydRunner`` drives it with the same sequence of
+calls as the reference's ``fit`` loop (kmeans_spark.py:266-318).  When the
+process is one rank of a multi-GPU job the statistics buffer is a torch
+tensor bound into the context and the context enqueues on a dedicated torch
+stream, so the RCCL all-reduce is stream-ordered between ``assign_stats`` and
+``update`` without host synchronisation.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+
+_PD = ctypes.POINTER(ctypes.c_double)
+_PF = ctypes.POINTER(ctypes.c_float)
+_PI32 = ctypes.POINTER(ctypes.c_int32)
+_PI64 = ctypes.POINTER(ctypes.c_int64)
+
+
+def _ptr(a: np.ndarray, t):
+    return a.ctypes.data_as(t)
+
+
+class HipEngine:
+    """A GPU context holding this rank's rows (no CPU fallback: raises if the
+    HIP extension or a gfx950 device is unavailable)."""
+
+    def __init__(self, device: int = 0, distributed: bool = False):
+        self.lib = _lib.load()
+        n = _lib.device_count()
+        if n <= 0:
+            raise _lib.KmError("no HIP device visible: the MI355X path needs a gfx950 GPU")
+        self.device = device
+        ctx = ctypes.c_void_p()
+        _lib.check(self.lib.km_create(device, ctypes.byref(ctx)), "km_create")
+        self.ctx = ctx
+        self.n = 0
+        self.d = 0
+        self.k = 0
+        self._stats_t = None
+        self._tstream = None
+        self.distributed = distributed
+        if distributed:
+            import torch
+            self._torch = torch
+            self._tstream = torch.cuda.Stream(device=f"cuda:{device}")
+            _lib.check(self.lib.km_set_stream(self.ctx, ctypes.c_void_p(self._tstream.cuda_stream)), "km_set_stream")
+
+    # -- lifetime --------------------------------------------------------------
+    def close(self):
+        if getattr(self, "ctx", None) is not None and self.ctx.value:
+            self.lib.km_destroy(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _c(self, rc, what):
+        return _lib.check(rc, what)
+
+    # -- data ------------------------------------------------------------------
+    def load_host(self, rows: np.ndarray) -> int:
+        """Copy this rank's rows (float32 [n][d]) into HBM once (rdd.cache(), L256)."""
+        rows = np.ascontiguousarray(rows, dtype=np.float32)
+        if rows.ndim != 2:
+            raise ValueError("rows must be a 2-D array")
+        n, d = rows.shape
+        self._c(self.lib.km_load_begin(self.ctx, n, d), "km_load_begin")
+        if n:
+            self._c(self.lib.km_load_rows(self.ctx, 0, _ptr(rows, _PF), n), "km_load_rows")
+        self.n, self.d = n, d
+        return n
+
+    def load_blobs(self, n: int, d: int, global_row0: int, n_centers: int, box: float = 10.0, std: float = 1.0,
+                   seed: int = 0) -> int:
+        self._c(self.lib.km_generate_blobs(self.ctx, n, d, global_row0, n_centers, box, std, seed),
+                "km_generate_blobs")
+        self.n, self.d = n, d
+        return n
+
+    def sum_x(self) -> np.ndarray:
+        out = np.zeros(self.d, dtype=np.float64)
+        self._c(self.lib.km_sum_x(self.ctx, _ptr(out, _PD)), "km_sum_x")
+        return out
+
+    def sq_dev(self, mu: np.ndarray) -> float:
+        mu = np.ascontiguousarray(mu, dtype=np.float64)
+        out = np.zeros(1, dtype=np.float64)
+        self._c(self.lib.km_sq_dev(self.ctx, _ptr(mu, _PD), _ptr(out, _PD)), "km_sq_dev")
+        return float(out[0])
+
+    def set_sse_base(self, v: float) -> None:
+        self._c(self.lib.km_set_sse_base(self.ctx, float(v)), "km_set_sse_base")
+
+    # -- centroids / iteration -------------------------------------------------
+    def set_centroids(self, C: np.ndarray) -> None:
+        C = np.ascontiguousarray(C, dtype=np.float64)
+        k, d = C.shape
+        self._c(self.lib.km_set_centroids(self.ctx, _ptr(C, _PD), k, d), "km_set_centroids")
+        if self.distributed and (self._stats_t is None or k != self.k):
+            torch = self._torch
+            self._stats_t = torch.zeros(k * (d + 1), dtype=torch.float64, device=f"cuda:{self.device}")
+            torch.cuda.synchronize(self.device)
+            self._c(self.lib.km_bind_stats_buffer(self.ctx, ctypes.c_void_p(self._stats_t.data_ptr())),
+                    "km_bind_stats_buffer")
+        self.k = k
+
+    def get_centroids(self, which: int = 0) -> np.ndarray:
+        out = np.empty((self.k, self.d), dtype=np.float64)
+        self._c(self.lib.km_get_centroids(self.ctx, which, _ptr(out, _PD)), "km_get_centroids")
+        return out
+
+    def assign_stats(self) -> None:
+        self._c(self.lib.km_assign_stats(self.ctx), "km_assign_stats")
+
+    def run_collective(self, fn) -> None:
+        """Run ``fn(stats_tensor)`` (an in-place all-reduce) ordered on this
+        context's stream."""
+        with self._torch.cuda.stream(self._tstream):
+            fn(self._stats_t)
+
+    def update(self) -> Tuple[_lib.KmStatus, np.ndarray]:
+        st = _lib.KmStatus()
+        counts = np.zeros(self.k, dtype=np.int64)
+        self._c(self.lib.km_update(self.ctx, ctypes.byref(st), _ptr(counts, _PI64)), "km_update")
+        return st, counts
+
+    def replace_rows(self, ids, rows: np.ndarray) -> None:
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        rows = np.ascontiguousarray(rows, dtype=np.float64).reshape(len(ids), self.d)
+        if len(ids):
+            self._c(self.lib.km_replace_rows(self.ctx, _ptr(ids, _PI32), _ptr(rows, _PD), len(ids)),
+                    "km_replace_rows")
+
+    def commit(self) -> None:
+        self._c(self.lib.km_commit(self.ctx), "km_commit")
+
+    def gather_rows(self, local_idx) -> np.ndarray:
+        idx = np.ascontiguousarray(local_idx, dtype=np.int64)
+        out = np.empty((len(idx), self.d), dtype=np.float64)
+        if len(idx):
+            self._c(self.lib.km_gather_rows(self.ctx, _ptr(idx, _PI64), len(idx), _ptr(out, _PD)),
+                    "km_gather_rows")
+        return out
+
+    def predict(self) -> np.ndarray:
+        out = np.empty(self.n, dtype=np.int32)
+        self._c(self.lib.km_predict(self.ctx, _ptr(out, _PI32)), "km_predict")
+        return out
+
+    def labels(self) -> np.ndarray:
+        out = np.empty(self.n, dtype=np.int32)
+        self._c(self.lib.km_labels(self.ctx, _ptr(out, _PI32)), "km_labels")
+        return out
+
+    def sync(self) -> None:
+        self._c(self.lib.km_sync(self.ctx), "km_sync")
+
+    def info(self) -> dict:
+        inf = _lib.KmInfo()
+        self._c(self.lib.km_info_get(self.ctx, ctypes.byref(inf)), "km_info_get")
+        return {f: getattr(inf, f) for f, _ in inf._fields_}
+
+    # -- profiling ---------------------------------------------------------------
+    def profile(self, enable: bool = True) -> None:
+        self._c(self.lib.km_profile(self.ctx, 1 if enable else 0), "km_profile")
+
+    def prof_read(self, kind: str) -> Tuple[float, int]:
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        self._c(self.lib.km_prof_read(self.ctx, _lib.KERNEL_KINDS[kind], ctypes.byref(ms), ctypes.byref(n)),
+                "km_prof_read")
+        return ms.value, n.value
+
+
+def make_engine(comm, device: Optional[int] = None) -> HipEngine:
+    dev = comm.local_rank if device is None else device
+    return HipEngine(dev, distributed=comm.world > 1)

@@ -1,0 +1,239 @@
+"""``KMeans`` — drop-in for the reference's class (kmeans_spark.py:19-352).
+
+Same constructor, attributes, messages, log lines and iteration order as the
+reference; the Lloyd iteration itself runs on the GPU (``engine.HipEngine``):
+
+  reference (PySpark)                         here
+  -------------------------------------       -----------------------------------------
+  rdd.cache()                      L256       rows copied to HBM once (engine.load_*)
+  sc.broadcast(centroids)          L268       centroids already resident (commit)
+  mapPartitions(assign_partition)  L161-171   km_assign_stats (screen + exact resolve + stats)
+  reduceByKey(..).collect()        L169-173   one RCCL all-reduce of the [k][d+1] stats
+  _update_centroids                L176-206   km_update (+ host empty-cluster repair)
+  _compute_sse                     L208-237   closed form from the same statistics
+  NaN check / shift / log / commit L289-313   identical, from the device status
+
+There is no CPU fallback: without the HIP extension or a gfx950 GPU, ``fit``
+and ``predict`` raise ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import sys
+import time
+from typing import List, Optional
+
+import numpy as np
+
+from . import sampling
+from .comm import Communicator
+from .dataset import DeviceBlobs, LocalRDD, Placement, place
+from .engine import make_engine
+
+
+class LloydRunner:
+    """Engine + data placement + communicator of one ``fit``; ``iteration``
+    performs one Lloyd iteration exactly as kmeans_spark.py:266-318."""
+
+    def __init__(self, engine, placement: Placement, comm: Communicator, k: int):
+        self.engine = engine
+        self.pl = placement
+        self.comm = comm
+        self.k = k
+        self.last = None
+
+    # -- set-up --------------------------------------------------------------------
+    def load(self) -> None:
+        pl = self.pl
+        if pl.blobs is not None:
+            b = pl.blobs
+            self.engine.load_blobs(pl.n_local, b.d, pl.row0, b.n_centers, b.box, b.std, b.seed)
+        else:
+            self.engine.load_host(pl.local_rows)
+        # data moments for the closed-form SSE (float64, global)
+        s = self.comm.allreduce_np(self.engine.sum_x())
+        mu = s / max(pl.n_global, 1)
+        a = self.comm.allreduce_np(np.array([self.engine.sq_dev(mu)]))[0]
+        self.engine.set_sse_base(a)
+
+    def rows(self, gidx: List[int]) -> np.ndarray:
+        """Rows by global index (what ``rdd.takeSample`` returns, L72/L196)."""
+        host = self.pl.host_rows(gidx)
+        if host is not None:
+            return host
+        gidx = np.asarray(gidx, dtype=np.int64)
+        lo, hi = self.pl.row0, self.pl.row0 + self.pl.n_local
+        mine = np.nonzero((gidx >= lo) & (gidx < hi))[0]
+        out = np.zeros((len(gidx), self.pl.d), dtype=np.float64)
+        if len(mine):
+            out[mine] = self.engine.gather_rows(gidx[mine] - lo)
+        return self.comm.allreduce_np(out)
+
+    # -- one Lloyd iteration -----------------------------------------------------------
+    def iteration(self, model: "KMeans", iteration: int, log) -> bool:
+        """Returns True when converged (max_shift < tolerance)."""
+        eng, k = self.engine, self.k
+        eng.assign_stats()                                     # L272 (+ L169-171 map side)
+        self.comm.allreduce_stats(eng)                         # L169-173 shuffle + collect
+        st, counts = eng.update()                              # L176-188 (+ SSE, shift)
+        max_shift = st.max_shift
+        nonfinite = bool(st.nonfinite)
+        if st.n_empty:                                         # L191
+            empty = [j for j in range(k) if counts[j] == 0]
+            log(f"  WARNING: {len(empty)} empty cluster(s) detected. Reinitializing...")
+            seed = self.comm.broadcast_obj(model._empty_seed())    # int(time.time()), L196
+            gidx = sampling.take_sample(self.pl.global_sizes, len(empty), seed)
+            reps = self.rows(gidx) if gidx else np.zeros((0, self.pl.d))
+            old = eng.get_centroids(0)
+            ids = empty[:len(reps)]                            # the rest keep the old centroid (L204)
+            if ids:
+                eng.replace_rows(ids, reps)
+                shift = np.linalg.norm(reps[:len(ids)] - old[ids], axis=1)
+                max_shift = max(max_shift, float(np.max(shift)))
+                nonfinite = nonfinite or not np.all(np.isfinite(reps))
+        sse = None
+        if model.compute_sse:                                  # L278-286
+            sse = float(st.sse)
+            model.sse_history.append(sse)
+            if len(model.sse_history) > 1 and sse > model.sse_history[-2] + 1e-6:
+                log(f"  WARNING: SSE increased from {model.sse_history[-2]:.4f} to {sse:.4f}")
+        if nonfinite:                                          # L289-290
+            raise ValueError(f"NaN or Inf detected in centroids at iteration {iteration + 1}")
+        cluster_sizes = [int(c) for c in counts]               # L297
+        if model.compute_sse and model.sse_history:
+            log(f"Iteration {iteration + 1}: SSE = {model.sse_history[-1]:.4f}, "
+                f"Max Shift = {max_shift:.6f}, Cluster Sizes = {cluster_sizes}")
+        else:
+            log(f"Iteration {iteration + 1}: Max Shift = {max_shift:.6f}, Cluster Sizes = {cluster_sizes}")
+        eng.commit()                                           # L307
+        self.last = {"max_shift": max_shift, "sse": sse, "counts": counts, "n_empty": int(st.n_empty),
+                     "q_rerank": int(st.q_rerank), "q_full": int(st.q_full)}
+        if max_shift < model.tolerance:                        # L310-313
+            log(f"Converged after {iteration + 1} iterations")
+            return True
+        return False
+
+
+class LabelsRDD(LocalRDD):
+    """``predict``'s result: an RDD-like of Python ints in input order."""
+
+    def __init__(self, local_labels: np.ndarray, comm: Communicator):
+        self._local = local_labels
+        self._comm = comm
+        self._all = None
+        super().__init__([])
+
+    def _gather(self) -> np.ndarray:
+        if self._all is None:
+            self._all = np.concatenate(self._comm.allgather_array(self._local)) if self._comm.world > 1 \
+                else self._local
+            self._parts = [self._all.tolist()]
+        return self._all
+
+    def collect(self) -> list:
+        return self._gather().tolist()
+
+    def count(self) -> int:
+        return int(len(self._gather()))
+
+    def getNumPartitions(self) -> int:
+        return 1
+
+    def to_numpy(self) -> np.ndarray:
+        return self._gather()
+
+
+class KMeans:
+    """Distributed K-Means, MI355X-native (kmeans_spark.py:19-47).
+
+    Parameters: k, max_iter, tolerance (max centroid shift), seed (sampling of
+    the initial centroids), compute_sse (track the SSE each iteration)."""
+
+    _engine_factory = None  # test seam: tests/ inject a CPU engine for host-logic tests
+
+    def __init__(self, k: int = 3, max_iter: int = 100, tolerance: float = 1e-4,
+                 seed: int = 42, compute_sse: bool = False):
+        self.k = k
+        self.max_iter = max_iter
+        self.tolerance = tolerance
+        self.seed = seed
+        self.compute_sse = compute_sse
+        self.centroids: np.ndarray = None
+        self.sse_history: List[float] = []
+        self._validate_parameters()
+        self.iterations_run = 0  # kept as the reference leaves it (never updated, L47)
+        self._runner: Optional[LloydRunner] = None
+        self._runner_key = None
+        self.verbose = True
+
+    def _validate_parameters(self):
+        if self.k <= 0:
+            raise ValueError(f"k must be positive, got {self.k}")
+        if self.max_iter <= 0:
+            raise ValueError(f"max_iter must be positive, got {self.max_iter}")
+        if self.tolerance <= 0:
+            raise ValueError(f"tolerance must be positive, got {self.tolerance}")
+
+    # -- hooks -----------------------------------------------------------------------
+    def _empty_seed(self) -> int:
+        return int(time.time())  # kmeans_spark.py:196
+
+    def _log(self, comm: Communicator):
+        def say(msg: str):
+            if self.verbose and comm.rank == 0:
+                print(msg)
+                sys.stdout.flush()
+        return say
+
+    def _make_runner(self, rdd, comm: Communicator) -> LloydRunner:
+        pl = place(rdd, comm)
+        factory = type(self)._engine_factory or make_engine
+        eng = factory(comm)
+        run = LloydRunner(eng, pl, comm, self.k)
+        run.load()
+        return run
+
+    def _initialize_centroids(self, run: LloydRunner) -> np.ndarray:
+        """kmeans_spark.py:58-82: k distinct rows by the takeSample policy."""
+        gidx = sampling.take_sample(run.pl.global_sizes, self.k, self.seed)
+        if len(gidx) < self.k:
+            raise ValueError(f"Not enough data points ({len(gidx)}) to initialize {self.k} clusters")
+        centroids = np.array(run.rows(gidx))
+        if not np.all(np.isfinite(centroids)):
+            raise ValueError("Data contains NaN or Inf values")
+        return centroids
+
+    # -- public API ----------------------------------------------------------------------
+    def fit(self, rdd, sc=None) -> "KMeans":
+        if hasattr(rdd, "cache"):
+            rdd.cache()                                        # L256
+        comm = Communicator()
+        run = self._make_runner(rdd, comm)
+        self._runner, self._runner_key = run, id(rdd)
+        self.centroids = self._initialize_centroids(run)       # L259
+        self.sse_history = []                                  # L260
+        say = self._log(comm)
+        say(f"Starting K-Means with k={self.k}, max_iter={self.max_iter}, tolerance={self.tolerance}")
+        say(f"SSE computation: {'ENABLED' if self.compute_sse else 'DISABLED (for performance)'}")
+        out_dtype = run.pl.dtype
+        run.engine.set_centroids(np.asarray(self.centroids, dtype=np.float64))
+        try:
+            for iteration in range(self.max_iter):             # L266
+                if run.iteration(self, iteration, say):
+                    break
+        finally:
+            self.centroids = run.engine.get_centroids(0).astype(out_dtype, copy=False)
+        return self
+
+    def predict(self, rdd, sc=None):
+        if self.centroids is None:
+            raise ValueError("Model must be fitted before prediction")
+        comm = Communicator()
+        if self._runner is not None and self._runner_key == id(rdd):
+            run = self._runner
+        else:
+            run = self._make_runner(rdd, comm)
+        run.engine.set_centroids(np.asarray(self.centroids, dtype=np.float64))
+        labels = LabelsRDD(run.engine.predict(), comm)
+        if sc is not None and hasattr(sc, "_jsc") and hasattr(rdd, "getNumPartitions"):
+            return sc.parallelize(labels.collect(), rdd.getNumPartitions())  # a real SparkContext
+        return labels

@@ -1,0 +1,186 @@
+"""Benchmark of the Lloyd-iteration hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+A "step" is one Lloyd iteration of ``KMeans.fit`` (assign -> partial stats ->
+RCCL all-reduce -> update -> commit, kmeans_spark.py:266-318) over the
+workload's rows, which were generated in HBM before timing.  Default workload
+= the metric's configuration, N=100M rows, d=64, k=256 (fits one MI355X: 25.6
+GB); the N rows are split over the ranks (strong scaling).  Rank 0 prints one
+JSON line with ``roofline`` (dominant kernel, HIP-event timed on its stream)
+and ``cpu_baseline`` (the oracle's per-point restatement of the reference
+closures, timed on this host on a bounded sample, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Lloyd iters/sec + points/sec, N=100M d=64 k=256, 1–8 GPUs; % of roofline"
+CONFIGS = {
+    # name: (N_total, d, k, n_centers)
+    "c3": (100_000_000, 64, 256, 256),
+    "c2": (10_000_000, 16, 8, 8),
+    "c4": (1_000_000_000, 32, 1024, 1024),
+    "c5": (50_000_000, 128, 4096, 4096),
+    "c3_small": (4_000_000, 64, 256, 256),
+}
+HBM_PEAK_GBS = 8000.0                 # MI355X spec (MI355X_MICROARCH.md)
+BF16_DENSE_TFLOPS = 2516.6            # dense bf16 MFMA peak
+BF16X3_EFFECTIVE_TFLOPS = BF16_DENSE_TFLOPS / 3.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work per worker")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                   help="per-launch HBM bytes from a rocprofv3 --pmc pass (optional)")
+    return p.parse_args()
+
+
+def init_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    return world, rank, local
+
+
+def cpu_baseline(d, k, n_total, seconds):
+    """The reference closure restated (oracle, per-point np.linalg.norm +
+    argmin + dict combine; kmeans_spark.py:147-173) on a bounded sample, one
+    process per worker, like Spark local[N]."""
+    from multiprocessing import get_context
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_baseline as cb
+    workers = max(1, min(16, os.cpu_count() or 1))
+    # calibrate points per worker for ~`seconds` of work
+    rate = cb.calibrate(d, k)
+    per = int(max(2000, min(400_000, rate * seconds)))
+    with get_context("spawn").Pool(workers) as pool:
+        t0 = time.perf_counter()
+        res = pool.starmap(cb.run_partition, [(d, k, per, w) for w in range(workers)])
+        dt = time.perf_counter() - t0
+    pts = sum(r[0] for r in res)
+    pps = pts / dt
+    return {"value": pps / n_total, "unit": f"Lloyd it/s (extrapolated to N={n_total:,})", "cores": workers,
+            "kind": "port", "points_per_sec": pps,
+            "sample": f"{workers} workers x {per} points, d={d}, k={k}, one assign+combine pass each "
+                      f"(oracle/cpu_baseline.py restating kmeans_spark.py:147-173); it/s = points/s / N"}
+
+
+def main():
+    args = parse()
+    world, rank, local = init_dist(args)
+    import kmeans_amd
+    from kmeans_amd.comm import Communicator
+
+    N, d, k, centers = CONFIGS[args.config]
+    comm = Communicator()
+    km = kmeans_amd.KMeans(k=k, max_iter=10 ** 9, tolerance=1e-300, seed=42, compute_sse=False)
+    km.verbose = False
+    data = kmeans_amd.DeviceBlobs(n=N, d=d, n_centers=centers, box=10.0, std=1.0, seed=2024)
+    run = km._make_runner(data, comm)
+    C0 = km._initialize_centroids(run)          # takeSample policy (L72), outside the timed region
+    eng = run.engine
+    eng.set_centroids(C0)
+    km.sse_history = []
+
+    def log(_msg):
+        pass
+
+    import torch
+    for i in range(args.warmup):
+        run.iteration(km, i, log)
+    eng.sync()
+    comm.barrier()
+    torch.cuda.synchronize()
+    eng.profile(True)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        run.iteration(km, args.warmup + i, log)
+    eng.sync()
+    torch.cuda.synchronize()
+    comm.barrier()
+    t1 = time.perf_counter()
+    eng.profile(False)
+    dt = float(comm.allreduce_np(np.array([t1 - t0])).max()) if world == 1 else None
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([t1 - t0], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    kern = {name: eng.prof_read(name) for name in ("assign", "resolve", "stats", "update", "prep")}
+    info = eng.info()
+    n_local = info["n"]
+    flops_launch = 2.0 * n_local * k * d                 # algorithmic distance contraction
+    bytes_stats = n_local * (d * 4 + 4)                  # X once + labels
+    bytes_assign = n_local * (d * 4 + 4)
+    dom = max(("assign", "stats"), key=lambda kk: kern[kk][0])
+    ms_dom, launches = kern[dom]
+    avg_s = (ms_dom / max(launches, 1)) / 1e3
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            tj = json.load(open(args.traffic))
+            if tj.get("config") == args.config and tj.get("kernel") == dom:
+                traffic = tj.get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    if info["path"] == 2 and dom == "assign":
+        ach = flops_launch / avg_s / 1e12
+        roof = {"bound": "mfma", "achieved": ach, "peak": BF16X3_EFFECTIVE_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / BF16X3_EFFECTIVE_TFLOPS, "traffic": traffic, "kernel": "k_assign_mfma (bf16x3)",
+                "peak_note": "dense bf16 MFMA 2516.6 TF / 3 (bf16x3 split); flops = 2*N*k*d per launch"}
+    else:
+        b = bytes_stats if dom == "stats" else bytes_assign
+        ach = b / avg_s / 1e9
+        roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                "traffic": traffic, "kernel": "k_stats" if dom == "stats" else "k_assign_small",
+                "bytes_note": "N*(d*4+4) per launch (rows once + labels)"}
+    kernel_ms = {kk: (v[0] / max(v[1], 1)) for kk, v in kern.items()}
+
+    if rank == 0:
+        it_s = args.steps / dt
+        out = {
+            "metric": METRIC, "value": it_s, "unit": "Lloyd it/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32 (bf16x3 MFMA screen, f64 exact resolve + stats)",
+            "data": "synthetic Gaussian blobs generated in HBM (centers U(-10,10), std 1)",
+            "config": {"workload": f"{args.config}: N={N} d={d} k={k}", "N": N, "d": d, "k": k,
+                       "parallelism": f"dp{world} (rows sharded, one RCCL all-reduce of k*(d+1) f64 per step)"},
+            "points_per_sec": N * it_s, "roofline": roof, "kernel_avg_ms": kernel_ms,
+            "resolve": {"q_rerank": run.last["q_rerank"], "q_full": run.last["q_full"]} if run.last else None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(d, k, N, args.cpu_seconds)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,151 @@
+/*
+ * kmeans_amd.h - C-ABI of the MI355X-native Lloyd-iteration hot path.
+ *
+ * Drop-in boundary for the reference's per-iteration worker closures and the
+ * Spark collectives around them (ersanjay16/Assignment--2-Group7-distributed-K-means,
+ * kmeans_spark.py).  The reference has no FFI of its own: its interface for
+ * this path is the PySpark RDD calls inside class KMeans, and each entry point
+ * below names the reference call it replaces.  The Python host layer
+ * (assignment--2-group7-distributed-k-means_amd/kmeans.py) binds these with
+ * ctypes and re-exposes the reference's KMeans(...)/fit(rdd, sc)/predict(rdd, sc)
+ * surface.
+ *
+ * Conventions
+ *   - every function returns int: 0 = OK (KM_OK), KM_EMPTY (>0) where noted,
+ *     < 0 = error; km_last_error() returns a thread-local message.
+ *   - plain C types only: host pointers are caller-owned and may be released
+ *     when the call returns; device pointers are marked "device".
+ *   - all matrices are row-major; centroids are float64 [k][d]; data rows are
+ *     float32 [n][d] (stored padded to a multiple of 16 features in HBM).
+ *   - one context = one GPU = one rank; a context is not thread-safe.
+ *   - work is enqueued on the context stream (km_set_stream, default: own
+ *     non-blocking stream); calls that return host data synchronise it.
+ */
+#ifndef KMEANS_AMD_H
+#define KMEANS_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KM_ABI_VERSION 1
+
+#define KM_OK 0
+#define KM_EMPTY 1          /* informational: the update found empty clusters */
+#define KM_ERR_ARG (-1)
+#define KM_ERR_HIP (-2)
+#define KM_ERR_STATE (-3)
+#define KM_ERR_UNSUPPORTED (-4)
+
+typedef struct km_ctx km_ctx;
+
+/* Per-iteration result of km_update (quantities of kmeans_spark.py:176-313). */
+typedef struct km_status {
+  double sse;        /* SSE of this assignment w.r.t. the pre-update centroids
+                        (replaces _compute_sse, kmeans_spark.py:208-237)        */
+  double max_shift;  /* max_c ||new_c - old_c||, empties counted as 0
+                        (kmeans_spark.py:293-294)                                */
+  int32_t n_empty;   /* clusters absent from the reduce (kmeans_spark.py:186-188) */
+  int32_t nonfinite; /* NaN/Inf in a new centroid (kmeans_spark.py:289)         */
+  int32_t q_rerank;  /* points whose top-2 were re-ranked in float64             */
+  int32_t q_full;    /* points that needed a full float64 scan                   */
+} km_status;
+
+/* Static facts about a context (for logging / benchmarks). */
+typedef struct km_info {
+  int64_t n;         /* local rows                                    */
+  int32_t d, dp;     /* features, padded row stride                   */
+  int32_t k, kp;     /* clusters, padded to a multiple of 32          */
+  int32_t path;      /* 1 = small direct-form path, 2 = MFMA bf16x3   */
+  int32_t n_cu;      /* compute units of the device                   */
+  int32_t device;
+  int32_t fused_stats;
+} km_info;
+
+/* Kernel kinds for km_prof_read. */
+#define KM_K_ASSIGN 0
+#define KM_K_RESOLVE 1
+#define KM_K_STATS 2
+#define KM_K_UPDATE 3
+#define KM_K_PREP 4
+#define KM_K_COUNT 5
+
+int km_abi_version(void);
+const char* km_last_error(void);
+int km_device_count(int* out);
+
+/* Context lifetime.  Replaces the SparkContext / executor set-up
+ * (kmeans_spark.py:626) for one GPU. */
+int km_create(int device, km_ctx** out);
+int km_destroy(km_ctx* ctx);
+/* Enqueue on an external stream (e.g. torch.cuda.current_stream()); NULL =
+ * the context's own stream. */
+int km_set_stream(km_ctx* ctx, void* hip_stream);
+int km_sync(km_ctx* ctx);
+int km_info_get(km_ctx* ctx, km_info* out);
+
+/* Materialise this rank's rows in HBM once: replaces sc.parallelize(X) +
+ * rdd.cache() (kmeans_spark.py:256, 369, 418, 471, 518, 568).  km_load_begin
+ * allocates n rows of d features; km_load_rows copies host float32 rows
+ * [row0, row0 + nrows) (pinned staging, chunked). */
+int km_load_begin(km_ctx* ctx, int64_t n, int32_t d);
+int km_load_rows(km_ctx* ctx, int64_t row0, const float* rows, int64_t nrows);
+/* Synthetic Gaussian blobs generated in HBM, keyed by global row (benchmarks). */
+int km_generate_blobs(km_ctx* ctx, int64_t n, int32_t d, int64_t global_row0, int32_t n_centers, float box,
+                      float stddev, uint64_t seed);
+/* Data moments for the SSE closed form: local sum_p x_p (float64 [d]); then,
+ * given the global mean mu, the local sum_p ||x_p - mu||^2; then the global
+ * value of that sum (all-reduced by the caller). */
+int km_sum_x(km_ctx* ctx, double* out_d);
+int km_sq_dev(km_ctx* ctx, const double* mu, double* out_local);
+int km_set_sse_base(km_ctx* ctx, double global_sq_dev);
+
+/* Set the current centroids: replaces sc.broadcast(self.centroids)
+ * (kmeans_spark.py:268, 340). */
+int km_set_centroids(km_ctx* ctx, const double* C, int32_t k, int32_t d);
+/* Read centroids: which = 0 current, 1 the update's new centroids. */
+int km_get_centroids(km_ctx* ctx, int32_t which, double* out);
+
+/* Assignment + partial statistics of one iteration: replaces
+ * rdd.mapPartitions(assign_partition) + the map-side combine of
+ * reduceByKey (kmeans_spark.py:147-171).  Output = the stats buffer
+ * (float64 [k][d+1]: per-cluster sum of x, then count). */
+int km_assign_stats(km_ctx* ctx);
+/* The stats buffer (device) and its length in doubles; a caller may bind an
+ * external device buffer instead (e.g. a torch tensor it all-reduces):
+ * this is the reduceByKey shuffle + collect (kmeans_spark.py:169-173). */
+int km_stats_buffer(km_ctx* ctx, void** dev_ptr, int64_t* len);
+int km_bind_stats_buffer(km_ctx* ctx, void* dev_ptr);
+
+/* Centroid update from the (all-reduced) stats: replaces _update_centroids
+ * (kmeans_spark.py:176-206), the SSE pass (:208-237, closed form) and the
+ * shift computation (:293-294).  Synchronises; fills *st and counts[k].
+ * Returns KM_EMPTY when clusters are empty (their new centroid is the old
+ * one until km_replace_rows). */
+int km_update(km_ctx* ctx, km_status* st, int64_t* counts);
+/* Empty-cluster repair (kmeans_spark.py:196-204): overwrite new centroids
+ * of the given clusters with the given rows (float64 [n][d]). */
+int km_replace_rows(km_ctx* ctx, const int32_t* cluster_ids, const double* rows, int32_t n);
+/* Commit the new centroids (kmeans_spark.py:307). */
+int km_commit(km_ctx* ctx);
+
+/* Rows by local index (float64 [n][d]): the rows behind rdd.takeSample
+ * (kmeans_spark.py:72, 196). */
+int km_gather_rows(km_ctx* ctx, const int64_t* local_idx, int32_t n, double* out);
+
+/* Labels of every local row for the current centroids: replaces predict's
+ * assign_partition (kmeans_spark.py:343-350). */
+int km_predict(km_ctx* ctx, int32_t* labels_out);
+/* Labels of the last km_assign_stats (device -> host). */
+int km_labels(km_ctx* ctx, int32_t* labels_out);
+
+/* Kernel timing with HIP events on the context stream. */
+int km_profile(km_ctx* ctx, int32_t enable);
+int km_prof_read(km_ctx* ctx, int32_t kind, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KMEANS_AMD_H */
