@@ -27,6 +27,13 @@ struct DevStatus {
   int32_t q_full;      // screened points that needed the full exact scan
 };
 
+// Per-wave segments of the ambiguous-point queue written by k_assign_mfma:
+// wave w owns entries [w*seg, w*seg + qcount[2w]); qcount[2w+1] = full scans.
+struct QLayout {
+  uint32_t seg;
+  uint32_t nwaves;
+};
+
 struct Geometry {
   int64_t n;    // local rows
   int32_t d;    // features
@@ -37,7 +44,7 @@ struct Geometry {
 
 // ---- launchers (km_kernels.hip) -------------------------------------------
 hipError_t launch_prep_centroids(const double* C64, const Geometry& g, float* C32, __bf16* Chi,
-                                 __bf16* Clo, float* cn2, float* cmax, hipStream_t s);
+                                 __bf16* Clo, float* cn2, float* cmax, double* C64T, hipStream_t s);
 // Small k*d path: direct-form fp32 screening, in-thread exact re-rank,
 // optional fused statistics (LDS float64 table, replicated per lane).
 hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C32, const double* C64,
@@ -48,15 +55,19 @@ bool small_path_ok(const Geometry& g);
 // ambiguous points queued for k_resolve.
 hipError_t launch_assign_mfma(const float* X, const Geometry& g, const __bf16* Chi, const __bf16* Clo,
                               const float* cn2, const float* cmax, int32_t* labels, QEntry* queue,
-                              uint32_t* qcount, int n_cu, hipStream_t s);
+                              uint32_t* qcount, int n_cu, QLayout* ql, hipStream_t s);
+// queue capacity (entries) and per-wave counter words needed for n rows
+size_t queue_capacity(int64_t n, int n_cu);
+size_t qcount_words(int n_cu);
 bool mfma_path_ok(const Geometry& g);
-hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const QEntry* queue,
-                          const uint32_t* qcount, int32_t* labels, int n_cu, hipStream_t s);
+hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
+                          const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels, int n_cu,
+                          hipStream_t s);
 hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels, double* stats, int n_cu,
                         hipStream_t s);
 hipError_t launch_update(const double* stats, const double* C64_old, const double* mu, const Geometry& g,
                          double* C64_new, double* work, int64_t* counts, const double* sse_base,
-                         const uint32_t* qcount, DevStatus* status, hipStream_t s);
+                         const uint32_t* qcount, uint32_t nq, DevStatus* status, hipStream_t s);
 hipError_t launch_sum_x(const float* X, const Geometry& g, double* out, hipStream_t s);
 hipError_t launch_sq_dev(const float* X, const Geometry& g, const double* mu, double* out, hipStream_t s);
 hipError_t launch_gather_rows(const float* X, const Geometry& g, const int64_t* idx, int32_t n, double* out,

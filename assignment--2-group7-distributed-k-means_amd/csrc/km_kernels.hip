@@ -11,6 +11,7 @@
 #include "km_internal.h"
 
 #include <float.h>
+#include <stdlib.h>
 
 namespace km {
 
@@ -28,7 +29,8 @@ __host__ __device__ inline int ceil_log2(int v) {
 
 // top-3 smallest keys, k1 <= k2 <= k3 (v_min_f32 + 2x v_med3_f32)
 __device__ __forceinline__ void top3_insert(float& k1, float& k2, float& k3, float v) {
-  const float n1 = fminf(k1, v);
+  // min as med3(k1, v, -FLT_MAX): no NaN-canonicalising v_max in front (fminf has one)
+  const float n1 = __builtin_amdgcn_fmed3f(k1, v, -FLT_MAX);
   const float n2 = __builtin_amdgcn_fmed3f(k1, k2, v);
   const float n3 = __builtin_amdgcn_fmed3f(k2, k3, v);
   k1 = n1;
@@ -93,12 +95,13 @@ __device__ inline float wave_sum_f(float v) {
 __global__ __launch_bounds__(64) void k_prep_centroids(const double* __restrict__ C64, int k, int d, int dp,
                                                        float* __restrict__ C32, __bf16* __restrict__ Chi,
                                                        __bf16* __restrict__ Clo, float* __restrict__ cn2,
-                                                       float* __restrict__ cmax) {
+                                                       float* __restrict__ cmax, double* __restrict__ C64T) {
   const int j = blockIdx.x;
   const int lane = threadIdx.x;
   double nn = 0.0;
   for (int f = lane; f < dp; f += 64) {
     const double c = (j < k && f < d) ? C64[(size_t)j * d + f] : 0.0;
+    if (j < k && f < d) C64T[(size_t)f * k + j] = c;
     nn = fma(c, c, nn);
     const float c32 = (float)c;
     C32[(size_t)j * dp + f] = c32;
@@ -119,10 +122,10 @@ __global__ __launch_bounds__(64) void k_prep_centroids(const double* __restrict_
 }
 
 hipError_t launch_prep_centroids(const double* C64, const Geometry& g, float* C32, __bf16* Chi, __bf16* Clo,
-                                 float* cn2, float* cmax, hipStream_t s) {
+                                 float* cn2, float* cmax, double* C64T, hipStream_t s) {
   hipError_t e = hipMemsetAsync(cmax, 0, sizeof(float), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_prep_centroids, dim3(g.kp), dim3(64), 0, s, C64, g.k, g.d, g.dp, C32, Chi, Clo, cn2, cmax);
+  hipLaunchKernelGGL(k_prep_centroids, dim3(g.kp), dim3(64), 0, s, C64, g.k, g.d, g.dp, C32, Chi, Clo, cn2, cmax, C64T);
   return hipGetLastError();
 }
 
@@ -289,8 +292,7 @@ hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C
 // (score | centroid index in the low mantissa bits) with min/med3.  The two
 // lane halves hold disjoint centroid rows and are merged at the end.
 // ---------------------------------------------------------------------------
-static constexpr int MFMA_LDS_SMALL = 80 * 1024;   // 2+ workgroups of 4 waves per CU
-static constexpr int MFMA_LDS_LARGE = 160 * 1024;  // 1 workgroup of 8 waves per CU
+static constexpr int MFMA_LDS_LARGE = 160 * 1024;  // LDS per CU
 
 template <int NS>
 __device__ __forceinline__ int phys_chunk(int c, int row) {
@@ -302,14 +304,36 @@ __device__ __forceinline__ int phys_chunk(int c, int row) {
   }
 }
 
+// Raw fp32 B-operand data of one 32-point tile: lane (r, h) holds features
+// [16s + 8h, 16s + 8h + 8) of point r for every K-step s.
+template <int NS>
+__device__ __forceinline__ void load_tile(const float* __restrict__ X, int64_t n, int64_t tile, int r, int h,
+                                          float4 (&xr)[2 * NS]) {
+  const int64_t row = tile * 32 + r;
+  const int64_t rl = row < n ? row : (n - 1);
+  const float* p = X + rl * (16 * NS) + 8 * h;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    xr[2 * s] = *reinterpret_cast<const float4*>(p + 16 * s);
+    xr[2 * s + 1] = *reinterpret_cast<const float4*>(p + 16 * s + 4);
+  }
+}
+
+// 8-wave workgroups; up to d = 64 two of them share a CU (4 waves per SIMD,
+// <= 128 VGPRs), wider rows get one (2 per SIMD).
 template <int NS, int WAVES>
-__global__ __launch_bounds__(WAVES * 64) void k_assign_mfma(const float* __restrict__ X, int64_t n, int k,
+constexpr int mfma_min_waves() {
+  return WAVES == 4 ? 1 : (NS <= 4 ? 4 : 2);
+}
+
+template <int NS, int WAVES, bool PF>
+__global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_assign_mfma(const float* __restrict__ X, int64_t n, int k,
                                                               int kp, const __bf16* __restrict__ Chi,
                                                               const __bf16* __restrict__ Clo,
                                                               const float* __restrict__ cn2,
                                                               const float* __restrict__ cmaxp,
                                                               int32_t* __restrict__ labels, QEntry* __restrict__ queue,
-                                                              uint32_t* __restrict__ qcount, int KC) {
+                                                              uint32_t* __restrict__ qcount, int KC, uint32_t seg) {
   constexpr int DP = 16 * NS;
   constexpr int ROWB = DP * 2;  // bytes per bf16 row
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -324,6 +348,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_assign_mfma(const float* __restr
   const int b = ceil_log2(kp);
   const uint32_t mask = (1u << b) - 1u;
   const float cm = *cmaxp;
+  // key truncation (index bits in the low mantissa), relative
+  const float rho = __builtin_ldexpf(1.0f, b - 23) * 1.01f;
   const int nchunks = (kp + KC - 1) / KC;
   const int64_t ntiles = (n + 31) / 32;
   const int64_t nwt = (ntiles + WAVES - 1) / WAVES;
@@ -348,20 +374,28 @@ __global__ __launch_bounds__(WAVES * 64) void k_assign_mfma(const float* __restr
     __syncthreads();
   }
 
-  for (int64_t wt = blockIdx.x; wt < nwt; wt += gridDim.x) {
+  // per-wave queue segment: no global counter (one hot address would
+  // serialise every wave at the memory side)
+  const uint32_t gw = blockIdx.x * WAVES + wave;
+  QEntry* wq = queue + (size_t)gw * seg;
+  uint32_t qn = 0, qf = 0;
+
+  float4 xr[2 * NS];
+  int64_t wt = blockIdx.x;
+  if (PF && wt < nwt) load_tile<NS>(X, n, wt * WAVES + wave, r, h, xr);
+  for (; wt < nwt; wt += gridDim.x) {
     const int64_t tile = wt * WAVES + wave;
     if (nchunks == 1 && tile >= ntiles) break;  // no barriers below in this mode
+    if (!PF) load_tile<NS>(X, n, tile, r, h, xr);
     const int64_t row = tile * 32 + r;
     const bool valid = row < n;
-    const int64_t rl = valid ? row : (n - 1);
-    const float* xr = X + rl * DP + 8 * h;
 
     bf16x8 bh[NS], bl[NS];
     float xx = 0.0f;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const float4 v0 = *reinterpret_cast<const float4*>(xr + 16 * s);
-      const float4 v1 = *reinterpret_cast<const float4*>(xr + 16 * s + 4);
+      const float4 v0 = xr[2 * s];
+      const float4 v1 = xr[2 * s + 1];
       const float xv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -372,8 +406,17 @@ __global__ __launch_bounds__(WAVES * 64) void k_assign_mfma(const float* __restr
       }
     }
     xx += __shfl_xor(xx, 32);
+    // software pipelining: the next tile's rows are in flight during this tile's MFMAs
+    if (PF && wt + gridDim.x < nwt) load_tile<NS>(X, n, (wt + gridDim.x) * WAVES + wave, r, h, xr);
 
-    float k1 = FLT_MAX, k2 = FLT_MAX, k3 = FLT_MAX;
+    // Four independent top-3 chains (ILP).  Chain c takes the accumulator
+    // registers reg = c, c+4, c+8, c+12, whose centroid index j has j & 3 == c,
+    // so a chain key stores only j >> 2 in its low mantissa bits (one v_bfi per
+    // score); the chain id is put back when the chains are merged.
+    const uint32_t maskq = mask >> 2;
+    float a1[4], a2[4], a3[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a1[c] = a2[c] = a3[c] = FLT_MAX;
     for (int ch = 0; ch < nchunks; ++ch) {
       if (nchunks > 1) {
         __syncthreads();
@@ -382,6 +425,14 @@ __global__ __launch_bounds__(WAVES * 64) void k_assign_mfma(const float* __restr
       }
       const int kc = min(KC, kp - ch * KC);
       for (int blk = 0; blk < kc / 32; ++blk) {
+        const int crow = blk * 32 + r;
+        bf16x8 ah[NS], al[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const size_t off = (size_t)crow * ROWB + (size_t)phys_chunk<NS>(2 * s + h, crow) * 16;
+          ah[s] = *reinterpret_cast<const bf16x8*>(sHi + off);
+          al[s] = *reinterpret_cast<const bf16x8*>(sLo + off);
+        }
         f32x16 acc;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
@@ -391,26 +442,36 @@ __global__ __launch_bounds__(WAVES * 64) void k_assign_mfma(const float* __restr
           acc[4 * g4 + 2] = cv.z;
           acc[4 * g4 + 3] = cv.w;
         }
-        const int crow = blk * 32 + r;
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-          const size_t off = (size_t)crow * ROWB + (size_t)phys_chunk<NS>(2 * s + h, crow) * 16;
-          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(sHi + off);
-          const bf16x8 al = *reinterpret_cast<const bf16x8*>(sLo + off);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bl[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s], bh[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bh[s], acc, 0, 0, 0);
         }
-        const uint32_t jb = (uint32_t)(ch * KC + blk * 32 + 4 * h);
+        // j = 32*blk + 4h + (reg & 3) + 8*(reg >> 2)  =>  j >> 2 = (8*blk + h) | 2*(reg >> 2)
+        const uint32_t jq = (uint32_t)((ch * KC + blk * 32) >> 2) + (uint32_t)h;
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
-          const uint32_t j = jb + (uint32_t)((reg & 3) + 8 * (reg >> 2));
-          top3_insert(k1, k2, k3, key_of(acc[reg], j, mask));
+          const uint32_t jf = jq | (uint32_t)(2 * (reg >> 2));
+          const float key = __uint_as_float((__float_as_uint(acc[reg]) & ~maskq) | jf);
+          top3_insert(a1[reg & 3], a2[reg & 3], a3[reg & 3], key);
         }
       }
     }
     if (nchunks > 1 && tile >= ntiles) continue;
 
+    // chain keys -> full-index keys: j = (field << 2) | c
+    auto full_key = [&](float kk, uint32_t c) -> float {
+      const uint32_t u = __float_as_uint(kk);
+      return __uint_as_float((u & ~mask) | ((((u & maskq) << 2) | c) & mask));
+    };
+    float k1 = full_key(a1[0], 0), k2 = full_key(a2[0], 0), k3 = full_key(a3[0], 0);
+#pragma unroll
+    for (int c = 1; c < 4; ++c) {
+      top3_insert(k1, k2, k3, full_key(a1[c], (uint32_t)c));
+      top3_insert(k1, k2, k3, full_key(a2[c], (uint32_t)c));
+      top3_insert(k1, k2, k3, full_key(a3[c], (uint32_t)c));
+    }
     // merge the two lane halves (disjoint centroid rows of the same point)
     {
       const float p1 = __shfl_xor(k1, 32);
@@ -420,54 +481,74 @@ __global__ __launch_bounds__(WAVES * 64) void k_assign_mfma(const float* __restr
       top3_insert(k1, k2, k3, p2);
       top3_insert(k1, k2, k3, p3);
     }
-    // rigorous screening bound on |S~ - S| (DESIGN.md "Exactness"), x2 safety
+    // Rigorous bound on |K_j - (||x - c_j||^2 - ||x||^2)| (DESIGN.md "Exactness"):
+    //   bf16x3 split residuals + fp32 accumulation + fp32 rounding of ||c||^2
+    //   (B0), plus the key truncation rho*|K| (index bits).
     const float xn = sqrtf(xx) * 1.0001f;
-    const float B0 = 2.0f * ((6.5f * U16 + (float)(6 * DP + 8) * U24) * xn * cm +
-                             (float)(3 * DP + 4) * U24 * cm * cm +
-                             __builtin_ldexpf(1.0f, b - 23) * (cm * cm + 2.0f * xn * cm));
+    const float B0 = 1.5f * ((6.5f * U16 + (float)(6 * DP + 8) * U24) * xn * cm +
+                             (float)(3 * DP + 4) * U24 * cm * cm + 4.0f * U24 * (xx + cm * cm + 2.0f * xn * cm));
+    // (2.5x on the far side: chain keys were selected at b-2 bits, re-keyed at b)
+    const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + 2.5f * fabsf(k3));
+    const float thr2 = 2.0f * B0 + rho * (fabsf(k1) + 2.5f * fabsf(k2));
     const uint32_t i1 = __float_as_uint(k1) & mask;
     const uint32_t i2 = __float_as_uint(k2) & mask;
     // negated tests: a NaN (non-finite data) falls through to the full float64
     // scan, whose np.argmin semantics then pick the first index
     uint32_t kind = 0;
-    if (!(k3 - k1 > 2.0f * B0))
+    if (!(k3 - k1 > thr3))
       kind = 2;
-    else if (!(k2 - k1 > 2.0f * B0))
+    else if (!(k2 - k1 > thr2))
       kind = 1;
     int lab = (i1 < (uint32_t)k) ? (int)i1 : 0;
     if (h == 0 && valid) labels[row] = lab;
     const bool enq = (h == 0) && valid && (kind != 0);
     const uint64_t m = __ballot(enq);
     if (m) {
-      const int cnt = __popcll(m);
-      const int leader = __ffsll((long long)m) - 1;
-      uint32_t base = 0;
-      if (lane == leader) base = atomicAdd(qcount, (uint32_t)cnt);
-      base = __shfl(base, leader);
+      // re-rank entries fill the wave's segment from the front, full scans
+      // from the back (resolved by different kernels)
+      const uint64_t m1 = __ballot(enq && kind == 1);
+      const uint64_t m2 = m & ~m1;
+      const uint64_t below = (1ull << lane) - 1ull;
       if (enq) {
-        const int pos = __popcll(m & ((1ull << lane) - 1ull));
         QEntry q;
         q.row = (uint32_t)row;
         q.i1 = i1;
         q.i2 = i2;
         q.kind = kind;
-        queue[base + pos] = q;
-        if (kind == 2) atomicAdd(qcount + 1, 1u);
+        const uint32_t pos = (kind == 1) ? qn + (uint32_t)__popcll(m1 & below)
+                                         : seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
+        wq[pos] = q;
       }
+      qn += (uint32_t)__popcll(m1);
+      qf += (uint32_t)__popcll(m2);
     }
+  }
+  if (lane == 0) {
+    qcount[2 * gw] = qn;
+    qcount[2 * gw + 1] = qf;
   }
 }
 
 static int mfma_kc(const Geometry& g, int* waves) {
   const size_t per = (size_t)g.dp * 4 + 4;
-  if ((size_t)g.kp * per <= MFMA_LDS_SMALL) {
-    *waves = 4;
-    return g.kp;
-  }
-  *waves = 8;
+  *waves = (g.dp >= 192) ? 4 : 8;
   if ((size_t)g.kp * per <= MFMA_LDS_LARGE) return g.kp;
   return (int)((MFMA_LDS_LARGE / per) / 32 * 32);
 }
+
+static bool mfma_prefetch() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("KM_MFMA_PREFETCH");  // default off: with 4 waves/SIMD the other waves hide it
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
+// at most 2 workgroups x 8 waves per CU, each wave's segment rounded up to
+// whole tiles: n + 32 * (waves) * 2 entries bound every layout
+size_t queue_capacity(int64_t n, int n_cu) { return (size_t)n + (size_t)32 * 16 * n_cu * 2 + 1024; }
+size_t qcount_words(int n_cu) { return (size_t)2 * 16 * n_cu + 16; }
 
 bool mfma_path_ok(const Geometry& g) {
   switch (g.dp) {
@@ -481,74 +562,231 @@ bool mfma_path_ok(const Geometry& g) {
 template <int NS>
 static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, const float* X, const Geometry& g,
                            const __bf16* Chi, const __bf16* Clo, const float* cn2, const float* cmax,
-                           int32_t* labels, QEntry* queue, uint32_t* qcount, int KC) {
-  if (waves == 4)
-    hipLaunchKernelGGL((k_assign_mfma<NS, 4>), dim3(blocks), dim3(256), lds, s, X, g.n, g.k, g.kp, Chi, Clo, cn2,
-                       cmax, labels, queue, qcount, KC);
-  else
-    hipLaunchKernelGGL((k_assign_mfma<NS, 8>), dim3(blocks), dim3(512), lds, s, X, g.n, g.k, g.kp, Chi, Clo, cn2,
-                       cmax, labels, queue, qcount, KC);
+                           int32_t* labels, QEntry* queue, uint32_t* qcount, int KC, uint32_t seg) {
+  if (waves == 4) {
+    hipLaunchKernelGGL((k_assign_mfma<NS, 4, true>), dim3(blocks), dim3(256), lds, s, X, g.n, g.k, g.kp, Chi, Clo,
+                       cn2, cmax, labels, queue, qcount, KC, seg);
+  } else if (mfma_prefetch()) {
+    hipLaunchKernelGGL((k_assign_mfma<NS, 8, true>), dim3(blocks), dim3(512), lds, s, X, g.n, g.k, g.kp, Chi, Clo,
+                       cn2, cmax, labels, queue, qcount, KC, seg);
+  } else {
+    hipLaunchKernelGGL((k_assign_mfma<NS, 8, false>), dim3(blocks), dim3(512), lds, s, X, g.n, g.k, g.kp, Chi, Clo,
+                       cn2, cmax, labels, queue, qcount, KC, seg);
+  }
 }
 
 hipError_t launch_assign_mfma(const float* X, const Geometry& g, const __bf16* Chi, const __bf16* Clo,
                               const float* cn2, const float* cmax, int32_t* labels, QEntry* queue,
-                              uint32_t* qcount, int n_cu, hipStream_t s) {
+                              uint32_t* qcount, int n_cu, QLayout* ql, hipStream_t s) {
+  ql->seg = 0;
+  ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
-  int waves = 4;
+  int waves = 8;
   const int KC = mfma_kc(g, &waves);
   if (KC < 32) return hipErrorInvalidValue;
   const size_t lds = 2 * (size_t)KC * g.dp * 2 + (size_t)KC * 4;
   const int64_t ntiles = (g.n + 31) / 32;
   const int64_t nwt = (ntiles + waves - 1) / waves;
-  const int per_cu = (waves == 4) ? (int)(MFMA_LDS_LARGE / lds > 4 ? 4 : MFMA_LDS_LARGE / lds) : 1;
-  int64_t blocks = (int64_t)n_cu * (per_cu < 1 ? 1 : per_cu);
+  int per_cu = (int)(MFMA_LDS_LARGE / lds);
+  const int max_per_cu = (waves == 4) ? 1 : (g.dp <= 64 ? 2 : 1);
+  if (per_cu > max_per_cu) per_cu = max_per_cu;
+  if (per_cu < 1) per_cu = 1;
+  int64_t blocks = (int64_t)n_cu * per_cu;
   if (blocks > nwt) blocks = nwt;
   const int nb = (int)blocks;
+  const uint32_t seg = (uint32_t)(((nwt + nb - 1) / nb) * 32);
+  ql->seg = seg;
+  ql->nwaves = (uint32_t)(nb * waves);
   switch (g.dp / 16) {
-    case 1: launch_mfma_ns<1>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC); break;
-    case 2: launch_mfma_ns<2>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC); break;
-    case 3: launch_mfma_ns<3>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC); break;
-    case 4: launch_mfma_ns<4>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC); break;
-    case 6: launch_mfma_ns<6>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC); break;
-    case 8: launch_mfma_ns<8>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC); break;
-    case 12: launch_mfma_ns<12>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC); break;
-    case 16: launch_mfma_ns<16>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC); break;
+    case 1: launch_mfma_ns<1>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
+    case 2: launch_mfma_ns<2>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
+    case 3: launch_mfma_ns<3>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
+    case 4: launch_mfma_ns<4>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
+    case 6: launch_mfma_ns<6>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
+    case 8: launch_mfma_ns<8>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
+    case 12: launch_mfma_ns<12>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
+    case 16: launch_mfma_ns<16>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
-// Exact float64 resolution of the queued ambiguous points.
+// Exact float64 resolution of the queued ambiguous points (np.argmin with
+// first-minimum tie-break, kmeans_spark.py:153-156).
+//   k_rerank2:   {i1, i2} re-ranked, 16 lanes per entry (4 entries per wave,
+//                float4 / double2 loads, all issued before use).
+//   k_fullscan:  full scan, one wave per entry, lanes over centroids, the
+//                transposed float64 centroids C64T[d][k] staged in LDS when
+//                they fit (read from L2 otherwise).
+// Walks the per-wave queue segments written by k_assign_mfma.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_resolve(const float* __restrict__ X, int dp, int d, int k,
+struct SegWalk {
+  const uint32_t* qcount;
+  uint32_t nseg, which;  // which: 0 = front counts (re-rank), 1 = back counts (full)
+  uint32_t sw = 0, sbase = 0, scnt = 0;
+  __device__ SegWalk(const uint32_t* q, uint32_t n, uint32_t w) : qcount(q), nseg(n), which(w) {
+    scnt = n ? q[w] : 0;
+  }
+  // map global entry number e (monotone per caller) to (segment, offset); false when past the end
+  __device__ bool locate(uint32_t e, uint32_t& seg_id, uint32_t& off) {
+    while (sw < nseg && e >= sbase + scnt) {
+      sbase += scnt;
+      ++sw;
+      scnt = (sw < nseg) ? qcount[2 * sw + which] : 0;
+    }
+    if (sw >= nseg) return false;
+    seg_id = sw;
+    off = e - sbase;
+    return true;
+  }
+};
+
+__global__ __launch_bounds__(256) void k_rerank2(const float* __restrict__ X, int dp, int d, int k,
                                                  const double* __restrict__ C64, const QEntry* __restrict__ queue,
-                                                 const uint32_t* __restrict__ qcount, int32_t* __restrict__ labels) {
-  const uint32_t cnt = qcount[0];
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
-    const QEntry q = queue[i];
-    const float* x = X + (size_t)q.row * dp;
-    int lab;
-    if (q.kind == 2 || q.i1 >= (uint32_t)k || q.i2 >= (uint32_t)k)
-      lab = exact_argmin(x, C64, k, d);
-    else
-      lab = exact_pick2(x, C64, d, (int)q.i1, (int)q.i2);
-    labels[q.row] = lab;
+                                                 const uint32_t* __restrict__ qcount, QLayout ql,
+                                                 int32_t* __restrict__ labels) {
+  const int lane = threadIdx.x & 63;
+  const int sub = lane >> 4;   // entry slot in the wave
+  const int m = lane & 15;     // features 4m..4m+3 (+64t)
+  const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+  SegWalk walk(qcount, ql.nwaves, 0);
+  for (uint32_t e0 = gw * 4;; e0 += nw * 4) {
+    uint32_t sg, off;
+    const bool have = walk.locate(e0 + sub, sg, off);
+    if (!__any(have)) {
+      // e0 + sub may cross a segment end while e0 + 3 is still inside: locate
+      // is monotone, so "no slot of this wave has an entry" means done
+      break;
+    }
+    QEntry q{0, 0, 0, 0};
+    if (have) q = queue[(size_t)sg * ql.seg + off];
+    const bool ok = have && q.i1 < (uint32_t)k && q.i2 < (uint32_t)k;
+    double s1 = 0.0, s2 = 0.0;
+    if (ok) {
+      const float* x = X + (size_t)q.row * dp;
+      const double* ca = C64 + (size_t)q.i1 * d;
+      const double* cb = C64 + (size_t)q.i2 * d;
+      for (int f0 = 4 * m; f0 < d; f0 += 64) {
+        const float4 xv = *reinterpret_cast<const float4*>(x + f0);
+        const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (f0 + c < d) {
+            const double xf = (double)xs[c];
+            const double ta = xf - ca[f0 + c];
+            const double tb = xf - cb[f0 + c];
+            s1 = fma(ta, ta, s1);
+            s2 = fma(tb, tb, s2);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) {
+      s1 += __shfl_xor(s1, o);
+      s2 += __shfl_xor(s2, o);
+    }
+    if (ok && m == 0) {
+      const bool first_a = q.i1 < q.i2;
+      const int a = (int)(first_a ? q.i1 : q.i2), bb = (int)(first_a ? q.i2 : q.i1);
+      const double sa = first_a ? s1 : s2, sb = first_a ? s2 : s1;
+      labels[q.row] = (sb < sa) ? bb : a;  // ties and NaN keep the lower index
+    } else if (have && !ok && m == 0) {
+      // corrupt candidate (cannot happen for finite data): exact scan
+      const float* x = X + (size_t)q.row * dp;
+      double best = 0.0;
+      int bl = 0;
+      for (int j = 0; j < k; ++j) {
+        double t2 = 0.0;
+        for (int f = 0; f < d; ++f) {
+          const double t = (double)x[f] - C64[(size_t)j * d + f];
+          t2 = fma(t, t, t2);
+        }
+        if (j == 0 || t2 < best) {
+          best = t2;
+          bl = j;
+        }
+      }
+      labels[q.row] = bl;
+    }
   }
 }
 
-hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const QEntry* queue,
-                          const uint32_t* qcount, int32_t* labels, int n_cu, hipStream_t s) {
-  if (g.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_resolve, dim3(n_cu * 2), dim3(256), 0, s, X, g.dp, g.d, g.k, C64, queue, qcount, labels);
+static constexpr int FULLSCAN_LDS = 152 * 1024;
+
+__global__ __launch_bounds__(256) void k_fullscan(const float* __restrict__ X, int dp, int d, int k,
+                                                  const double* __restrict__ C64T, const QEntry* __restrict__ queue,
+                                                  const uint32_t* __restrict__ qcount, QLayout ql,
+                                                  int32_t* __restrict__ labels, int use_lds) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sCT = reinterpret_cast<double*>(smem);
+  if (use_lds) {
+    for (int i = threadIdx.x; i < k * d; i += blockDim.x) sCT[i] = C64T[i];
+    __syncthreads();
+  }
+  const double* CT = use_lds ? sCT : C64T;
+  const int lane = threadIdx.x & 63;
+  const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+  SegWalk walk(qcount, ql.nwaves, 1);
+  for (uint32_t e = gw;; e += nw) {
+    uint32_t sg, off;
+    if (!walk.locate(e, sg, off)) break;
+    const QEntry* qp = queue + (size_t)sg * ql.seg + (ql.seg - 1u - off);
+    const uint32_t row = __builtin_amdgcn_readfirstlane(qp->row);
+    const float* x = X + (size_t)row * dp;
+    double best = 0.0;
+    int bj = 0x7fffffff;
+    for (int j0 = 0; j0 < k; j0 += 64) {
+      const int j = j0 + lane;
+      if (j < k) {
+        double acc = 0.0;
+        for (int f = 0; f < d; ++f) {
+          const double t = (double)x[f] - CT[(size_t)f * k + j];
+          acc = fma(t, t, acc);
+        }
+        if (!(acc != acc) && (bj == 0x7fffffff || acc < best)) {
+          best = acc;
+          bj = j;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double ob = __shfl_xor(best, o);
+      const int oj = __shfl_xor(bj, o);
+      if (oj != 0x7fffffff && (bj == 0x7fffffff || ob < best || (ob == best && oj < bj))) {
+        best = ob;
+        bj = oj;
+      }
+    }
+    if (lane == 0) labels[row] = (bj == 0x7fffffff) ? 0 : bj;  // all-NaN distances: np.argmin -> 0
+  }
+}
+
+hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
+                          const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels, int n_cu,
+                          hipStream_t s) {
+  if (g.n == 0 || ql.nwaves == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rerank2, dim3(n_cu * 8), dim3(256), 0, s, X, g.dp, g.d, g.k, C64, queue, qcount, ql, labels);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t bytes = (size_t)g.k * g.d * 8;
+  const int use_lds = bytes <= FULLSCAN_LDS ? 1 : 0;
+  hipLaunchKernelGGL(k_fullscan, dim3(n_cu), dim3(256), use_lds ? bytes : 0, s, X, g.dp, g.d, g.k, C64T, queue,
+                     qcount, ql, labels, use_lds);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
 // Partial statistics (reduceByKey, kmeans_spark.py:169-173): per cluster
 // sum of x and count, float64, into an LDS table; a workgroup owns a range of
-// clusters (blockIdx.y) and a range of rows (blockIdx.x); one float64 global
-// atomic per non-zero table entry at the end.
+// clusters (blockIdx.y) and a range of rows (blockIdx.x); a wave streams
+// chunks of 64 contiguous rows as coalesced float4 loads (8 in flight per
+// lane), labels broadcast from one coalesced load; one float64 global atomic
+// per non-zero table entry at the end.
 // ---------------------------------------------------------------------------
 static constexpr int STATS_LDS = 156 * 1024;
 
@@ -557,10 +795,14 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
                                                 int kr, int64_t rows_per_block) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* tab = reinterpret_cast<double*>(smem);
-  const int d1 = d + 1;
+  // LDS row of a cluster: dp feature slots + count.  Feature f = 4m + c of a
+  // row is stored at slot c*L + m (L = dp/4 lanes per row), so the 4 atomics
+  // of a float4 each hit L consecutive doubles: no bank conflicts.
+  const int RS = dp + 1;
+  const int L = dp / 4;
   const int c0 = blockIdx.y * kr;
   const int c1 = min(k, c0 + kr);
-  const int nent = (c1 - c0) * d1;
+  const int nent = (c1 - c0) * RS;
   for (int i = threadIdx.x; i < nent; i += blockDim.x) tab[i] = 0.0;
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
@@ -568,58 +810,73 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int nwaves = blockDim.x >> 6;
-  int dpp = 1;
-  while (dpp < d1) dpp <<= 1;
-  if (dpp <= 64) {
-    const int P = 64 / dpp;
-    const int q = lane / dpp;
-    const int f = lane % dpp;
-    for (int64_t base = r0 + (int64_t)wave * P; base < r1; base += (int64_t)nwaves * P) {
-      const int64_t row = base + q;
-      if (row < r1 && f < d1) {
-        const int lab = labels[row];
-        if (lab >= c0 && lab < c1) {
-          const float v = (f < d) ? X[row * dp + f] : 1.0f;
-          atomicAdd(tab + (lab - c0) * d1 + f, (double)v);
-        }
+  const int P = 64 / L;        // rows per load instruction (L <= 64)
+  const int q = lane / L;
+  const int mm = lane % L;
+  constexpr int U = 8;         // float4 loads in flight per lane
+  for (int64_t cr = r0 + (int64_t)wave * 64; cr < r1; cr += (int64_t)nwaves * 64) {
+    const int nrow = (int)min((int64_t)64, r1 - cr);
+    const int labreg = lane < nrow ? labels[cr + lane] : -1;
+    if (lane < nrow && labreg >= c0 && labreg < c1) atomicAdd(tab + (labreg - c0) * RS + dp, 1.0);  // counts
+    const float4* base = reinterpret_cast<const float4*>(X + cr * dp);
+    for (int rb = 0; rb < nrow; rb += P * U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rr = rb + u * P + q;
+        v[u] = rr < nrow ? base[(size_t)rr * L + mm] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-    }
-  } else {
-    for (int64_t row = r0 + wave; row < r1; row += nwaves) {
-      const int lab = labels[row];
-      if (lab >= c0 && lab < c1) {
-        double* t = tab + (lab - c0) * d1;
-        for (int f = lane; f < d1; f += 64) {
-          const float v = (f < d) ? X[row * dp + f] : 1.0f;
-          atomicAdd(t + f, (double)v);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rr = rb + u * P + q;
+        const int lab = __shfl(labreg, rr & 63);
+        if (rr < nrow && lab >= c0 && lab < c1) {
+          double* t = tab + (lab - c0) * RS + mm;
+          atomicAdd(t, (double)v[u].x);
+          atomicAdd(t + L, (double)v[u].y);
+          atomicAdd(t + 2 * L, (double)v[u].z);
+          atomicAdd(t + 3 * L, (double)v[u].w);
         }
       }
     }
   }
   __syncthreads();
+  const int d1 = d + 1;
   for (int i = threadIdx.x; i < nent; i += blockDim.x) {
+    const int j = i / RS;
+    const int p = i - j * RS;
     const double v = tab[i];
-    if (v != 0.0) atomicAdd(stats + (size_t)c0 * d1 + i, v);
+    if (v == 0.0) continue;
+    int f;
+    if (p == dp) {
+      f = d;  // count
+    } else {
+      f = 4 * (p % L) + p / L;
+      if (f >= d) continue;  // zero padding
+    }
+    atomicAdd(stats + (size_t)(c0 + j) * d1 + f, v);
   }
 }
 
 hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels, double* stats, int n_cu,
                         hipStream_t s) {
   if (g.n == 0) return hipSuccess;
-  const int d1 = g.d + 1;
-  int kr = (int)(STATS_LDS / ((size_t)d1 * 8));
+  const int RS = g.dp + 1;
+  if (g.dp > 256 || g.dp % 4) return hipErrorInvalidValue;
+  int kr = (int)(STATS_LDS / ((size_t)RS * 8));
   if (kr < 1) return hipErrorInvalidValue;
   if (kr > g.k) kr = g.k;
   const int ranges = (g.k + kr - 1) / kr;
-  const size_t lds = (size_t)kr * d1 * 8;
+  const size_t lds = (size_t)kr * RS * 8;
   int per_cu = (int)((160 * 1024) / (lds + 1024));
   if (per_cu < 1) per_cu = 1;
   if (per_cu > 2) per_cu = 2;
   int64_t bx = (int64_t)n_cu * per_cu / ranges;
   if (bx < 1) bx = 1;
-  const int64_t min_rows = 2048;
+  const int64_t min_rows = 4096;
   if (bx > (g.n + min_rows - 1) / min_rows) bx = (g.n + min_rows - 1) / min_rows;
-  const int64_t rpb = (g.n + bx - 1) / bx;
+  int64_t rpb = (g.n + bx - 1) / bx;
+  rpb = (rpb + 63) / 64 * 64;
   hipLaunchKernelGGL(k_stats, dim3((unsigned)bx, (unsigned)ranges), dim3(1024), lds, s, X, g.n, g.d, g.dp, g.k,
                      labels, stats, kr, rpb);
   return hipGetLastError();
@@ -667,11 +924,18 @@ __global__ __launch_bounds__(64) void k_update(const double* __restrict__ stats,
 
 __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ work, const int64_t* __restrict__ counts,
                                                   int k, const double* __restrict__ sse_base,
-                                                  const uint32_t* __restrict__ qcount, DevStatus* __restrict__ st) {
+                                                  const uint32_t* __restrict__ qcount, uint32_t nq,
+                                                  DevStatus* __restrict__ st) {
   __shared__ double s_max[256], s_sum[256];
-  __shared__ int s_emp[256], s_nf[256];
+  __shared__ int s_emp[256], s_nf[256], s_q[256], s_qf[256];
   double mx = 0.0, sm = 0.0;
-  int emp = 0, nf = 0;
+  int emp = 0, nf = 0, qa = 0, qb = 0;
+  for (uint32_t w = threadIdx.x; w < nq; w += 256) {
+    qa += (int)qcount[2 * w];
+    qb += (int)qcount[2 * w + 1];
+  }
+  s_q[threadIdx.x] = qa;
+  s_qf[threadIdx.x] = qb;
   for (int j = threadIdx.x; j < k; j += 256) {
     mx = fmax(mx, work[j]);
     sm += work[k + j];
@@ -689,6 +953,8 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ wor
       s_sum[threadIdx.x] += s_sum[threadIdx.x + o];
       s_emp[threadIdx.x] += s_emp[threadIdx.x + o];
       s_nf[threadIdx.x] |= s_nf[threadIdx.x + o];
+      s_q[threadIdx.x] += s_q[threadIdx.x + o];
+      s_qf[threadIdx.x] += s_qf[threadIdx.x + o];
     }
     __syncthreads();
   }
@@ -697,18 +963,18 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ wor
     st->sse = *sse_base + s_sum[0];
     st->n_empty = s_emp[0];
     st->nonfinite = s_nf[0];
-    st->q_full = (int32_t)qcount[1];
-    st->q_rerank = (int32_t)(qcount[0] - qcount[1]);
+    st->q_full = s_qf[0];
+    st->q_rerank = s_q[0];
   }
 }
 
 hipError_t launch_update(const double* stats, const double* C64_old, const double* mu, const Geometry& g,
                          double* C64_new, double* work, int64_t* counts, const double* sse_base,
-                         const uint32_t* qcount, DevStatus* status, hipStream_t s) {
+                         const uint32_t* qcount, uint32_t nq, DevStatus* status, hipStream_t s) {
   hipLaunchKernelGGL(k_update, dim3(g.k), dim3(64), 0, s, stats, C64_old, mu, g.k, g.d, C64_new, work, counts);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, work, counts, g.k, sse_base, qcount, status);
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, work, counts, g.k, sse_base, qcount, nq, status);
   return hipGetLastError();
 }
 

@@ -68,6 +68,7 @@ struct km_ctx {
   int32_t* labels = nullptr;
   km::QEntry* queue = nullptr;
   uint32_t* qcount = nullptr;
+  km::QLayout ql{0, 0};
   double* moments = nullptr;  // d+1 scratch
   double* mu = nullptr;       // d
   double* sse_base = nullptr; // 1
@@ -78,6 +79,7 @@ struct km_ctx {
   int k_alloc = 0;
   double* C64_cur = nullptr;
   double* C64_new = nullptr;
+  double* C64T = nullptr;  // transposed [d][k] (full exact scans)
   float* C32 = nullptr;
   __bf16* Chi = nullptr;
   __bf16* Clo = nullptr;
@@ -134,6 +136,7 @@ struct ProfScope {
 void free_centroids(km_ctx* c) {
   dfree(c->C64_cur);
   dfree(c->C64_new);
+  dfree(c->C64T);
   dfree(c->C32);
   dfree(c->Chi);
   dfree(c->Clo);
@@ -169,7 +172,7 @@ void free_data(km_ctx* c) {
 
 int prep(km_ctx* c) {
   ProfScope ps(c, KM_K_PREP);
-  KM_HIP(km::launch_prep_centroids(c->C64_cur, c->g, c->C32, c->Chi, c->Clo, c->cn2, c->cmax, c->stream));
+  KM_HIP(km::launch_prep_centroids(c->C64_cur, c->g, c->C32, c->Chi, c->Clo, c->cn2, c->cmax, c->C64T, c->stream));
   return KM_OK;
 }
 
@@ -185,7 +188,7 @@ int ensure_scratch(km_ctx* c, int64_t rows) {
 
 int run_assign(km_ctx* c, bool with_stats) {
   const km::Geometry& g = c->g;
-  KM_HIP(hipMemsetAsync(c->qcount, 0, 4 * sizeof(uint32_t), c->stream));
+  c->ql = km::QLayout{0, 0};
   if (with_stats) KM_HIP(hipMemsetAsync(c->stats, 0, sizeof(double) * (size_t)g.k * (g.d + 1), c->stream));
   if (c->path == 1) {
     ProfScope ps(c, KM_K_ASSIGN);
@@ -196,11 +199,11 @@ int run_assign(km_ctx* c, bool with_stats) {
   {
     ProfScope ps(c, KM_K_ASSIGN);
     KM_HIP(km::launch_assign_mfma(c->X, g, c->Chi, c->Clo, c->cn2, c->cmax, c->labels, c->queue, c->qcount, c->n_cu,
-                                  c->stream));
+                                  &c->ql, c->stream));
   }
   {
     ProfScope ps(c, KM_K_RESOLVE);
-    KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->queue, c->qcount, c->labels, c->n_cu, c->stream));
+    KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels, c->n_cu, c->stream));
   }
   if (with_stats) {
     ProfScope ps(c, KM_K_STATS);
@@ -314,8 +317,8 @@ int km_load_begin(km_ctx* c, int64_t n, int32_t d) {
   KM_HIP(hipMalloc(&c->X, sizeof(float) * rows * c->g.dp));
   KM_HIP(hipMemsetAsync(c->X, 0, sizeof(float) * rows * c->g.dp, c->stream));
   KM_HIP(hipMalloc(&c->labels, sizeof(int32_t) * rows));
-  KM_HIP(hipMalloc(&c->queue, sizeof(km::QEntry) * rows));
-  KM_HIP(hipMalloc(&c->qcount, 4 * sizeof(uint32_t)));
+  KM_HIP(hipMalloc(&c->queue, sizeof(km::QEntry) * km::queue_capacity(rows, c->n_cu)));
+  KM_HIP(hipMalloc(&c->qcount, sizeof(uint32_t) * km::qcount_words(c->n_cu)));
   KM_HIP(hipMalloc(&c->moments, sizeof(double) * (d + 1)));
   KM_HIP(hipMalloc(&c->mu, sizeof(double) * d));
   KM_HIP(hipMemsetAsync(c->mu, 0, sizeof(double) * d, c->stream));
@@ -406,6 +409,7 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
     const int kp = c->g.kp, dp = c->g.dp;
     KM_HIP(hipMalloc(&c->C64_cur, sizeof(double) * k * d));
     KM_HIP(hipMalloc(&c->C64_new, sizeof(double) * k * d));
+    KM_HIP(hipMalloc(&c->C64T, sizeof(double) * k * d));
     KM_HIP(hipMalloc(&c->C32, sizeof(float) * kp * dp));
     KM_HIP(hipMalloc(&c->Chi, sizeof(__bf16) * kp * dp));
     KM_HIP(hipMalloc(&c->Clo, sizeof(__bf16) * kp * dp));
@@ -470,7 +474,7 @@ int km_update(km_ctx* c, km_status* st, int64_t* counts) {
   {
     ProfScope ps(c, KM_K_UPDATE);
     KM_HIP(km::launch_update(c->stats, c->C64_cur, c->mu, c->g, c->C64_new, c->work, c->counts_dev, c->sse_base,
-                             c->qcount, c->status_dev, c->stream));
+                             c->qcount, c->ql.nwaves, c->status_dev, c->stream));
   }
   KM_HIP(hipMemcpyAsync(c->status_host, c->status_dev, sizeof(km::DevStatus), hipMemcpyDeviceToHost, c->stream));
   KM_HIP(hipMemcpyAsync(c->counts_host, c->counts_dev, sizeof(int64_t) * c->g.k, hipMemcpyDeviceToHost, c->stream));
