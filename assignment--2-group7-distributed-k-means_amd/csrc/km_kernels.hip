@@ -621,27 +621,6 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const __bf16* C
 //                they fit (read from L2 otherwise).
 // Walks the per-wave queue segments written by k_assign_mfma.
 // ---------------------------------------------------------------------------
-struct SegWalk {
-  const uint32_t* qcount;
-  uint32_t nseg, which;  // which: 0 = front counts (re-rank), 1 = back counts (full)
-  uint32_t sw = 0, sbase = 0, scnt = 0;
-  __device__ SegWalk(const uint32_t* q, uint32_t n, uint32_t w) : qcount(q), nseg(n), which(w) {
-    scnt = n ? q[w] : 0;
-  }
-  // map global entry number e (monotone per caller) to (segment, offset); false when past the end
-  __device__ bool locate(uint32_t e, uint32_t& seg_id, uint32_t& off) {
-    while (sw < nseg && e >= sbase + scnt) {
-      sbase += scnt;
-      ++sw;
-      scnt = (sw < nseg) ? qcount[2 * sw + which] : 0;
-    }
-    if (sw >= nseg) return false;
-    seg_id = sw;
-    off = e - sbase;
-    return true;
-  }
-};
-
 __global__ __launch_bounds__(256) void k_rerank2(const float* __restrict__ X, int dp, int d, int k,
                                                  const double* __restrict__ C64, const QEntry* __restrict__ queue,
                                                  const uint32_t* __restrict__ qcount, QLayout ql,
@@ -651,65 +630,65 @@ __global__ __launch_bounds__(256) void k_rerank2(const float* __restrict__ X, in
   const int m = lane & 15;     // features 4m..4m+3 (+64t)
   const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
-  SegWalk walk(qcount, ql.nwaves, 0);
-  for (uint32_t e0 = gw * 4;; e0 += nw * 4) {
-    uint32_t sg, off;
-    const bool have = walk.locate(e0 + sub, sg, off);
-    if (!__any(have)) {
-      // e0 + sub may cross a segment end while e0 + 3 is still inside: locate
-      // is monotone, so "no slot of this wave has an entry" means done
-      break;
-    }
-    QEntry q{0, 0, 0, 0};
-    if (have) q = queue[(size_t)sg * ql.seg + off];
-    const bool ok = have && q.i1 < (uint32_t)k && q.i2 < (uint32_t)k;
-    double s1 = 0.0, s2 = 0.0;
-    if (ok) {
-      const float* x = X + (size_t)q.row * dp;
-      const double* ca = C64 + (size_t)q.i1 * d;
-      const double* cb = C64 + (size_t)q.i2 * d;
-      for (int f0 = 4 * m; f0 < d; f0 += 64) {
-        const float4 xv = *reinterpret_cast<const float4*>(x + f0);
-        const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+  // every assign wave wrote about the same number of entries: one resolve
+  // wave per segment (grid-stride), 4 entries per wave-iteration
+  for (uint32_t sg = gw; sg < ql.nwaves; sg += nw) {
+    const uint32_t cnt = qcount[2 * sg];
+    const QEntry* qs = queue + (size_t)sg * ql.seg;
+    for (uint32_t e0 = 0; e0 < cnt; e0 += 4) {
+      const uint32_t e = e0 + (uint32_t)sub;
+      const bool have = e < cnt;
+      QEntry q{0, 0, 0, 0};
+      if (have) q = qs[e];
+      const bool ok = have && q.i1 < (uint32_t)k && q.i2 < (uint32_t)k;
+      double s1 = 0.0, s2 = 0.0;
+      if (ok) {
+        const float* x = X + (size_t)q.row * dp;
+        const double* ca = C64 + (size_t)q.i1 * d;
+        const double* cb = C64 + (size_t)q.i2 * d;
+        for (int f0 = 4 * m; f0 < d; f0 += 64) {
+          const float4 xv = *reinterpret_cast<const float4*>(x + f0);
+          const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          if (f0 + c < d) {
-            const double xf = (double)xs[c];
-            const double ta = xf - ca[f0 + c];
-            const double tb = xf - cb[f0 + c];
-            s1 = fma(ta, ta, s1);
-            s2 = fma(tb, tb, s2);
+          for (int c = 0; c < 4; ++c) {
+            if (f0 + c < d) {
+              const double xf = (double)xs[c];
+              const double ta = xf - ca[f0 + c];
+              const double tb = xf - cb[f0 + c];
+              s1 = fma(ta, ta, s1);
+              s2 = fma(tb, tb, s2);
+            }
           }
         }
       }
-    }
 #pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) {
-      s1 += __shfl_xor(s1, o);
-      s2 += __shfl_xor(s2, o);
-    }
-    if (ok && m == 0) {
-      const bool first_a = q.i1 < q.i2;
-      const int a = (int)(first_a ? q.i1 : q.i2), bb = (int)(first_a ? q.i2 : q.i1);
-      const double sa = first_a ? s1 : s2, sb = first_a ? s2 : s1;
-      labels[q.row] = (sb < sa) ? bb : a;  // ties and NaN keep the lower index
-    } else if (have && !ok && m == 0) {
-      // corrupt candidate (cannot happen for finite data): exact scan
-      const float* x = X + (size_t)q.row * dp;
-      double best = 0.0;
-      int bl = 0;
-      for (int j = 0; j < k; ++j) {
-        double t2 = 0.0;
-        for (int f = 0; f < d; ++f) {
-          const double t = (double)x[f] - C64[(size_t)j * d + f];
-          t2 = fma(t, t, t2);
-        }
-        if (j == 0 || t2 < best) {
-          best = t2;
-          bl = j;
-        }
+      for (int o = 8; o >= 1; o >>= 1) {
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
       }
-      labels[q.row] = bl;
+      if (ok && m == 0) {
+        const bool first_a = q.i1 < q.i2;
+        const int a = (int)(first_a ? q.i1 : q.i2), bb = (int)(first_a ? q.i2 : q.i1);
+        const double sa = first_a ? s1 : s2, sb = first_a ? s2 : s1;
+        labels[q.row] = (sb < sa) ? bb : a;  // ties and NaN keep the lower index
+      } else if (have && !ok && m == 0) {
+        // corrupt candidate (cannot happen for finite data): exact scan
+        const float* x = X + (size_t)q.row * dp;
+        double best = 0.0;
+        int bl = 0;
+        for (int j = 0; j < k; ++j) {
+          double t2 = 0.0;
+          for (int f = 0; f < d; ++f) {
+            const double t = (double)x[f] - C64[(size_t)j * d + f];
+            t2 = fma(t, t, t2);
+          }
+          if (j == 0 || t2 < best) {
+            best = t2;
+            bl = j;
+          }
+        }
+        labels[q.row] = bl;
+      }
     }
   }
 }
@@ -730,11 +709,12 @@ __global__ __launch_bounds__(256) void k_fullscan(const float* __restrict__ X, i
   const int lane = threadIdx.x & 63;
   const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
-  SegWalk walk(qcount, ql.nwaves, 1);
-  for (uint32_t e = gw;; e += nw) {
-    uint32_t sg, off;
-    if (!walk.locate(e, sg, off)) break;
-    const QEntry* qp = queue + (size_t)sg * ql.seg + (ql.seg - 1u - off);
+  // one wave per segment (grid-stride); each segment's full-scan entries sit
+  // at its back
+  for (uint32_t sg = gw; sg < ql.nwaves; sg += nw) {
+   const uint32_t cnt = qcount[2 * sg + 1];
+   for (uint32_t e = 0; e < cnt; ++e) {
+    const QEntry* qp = queue + (size_t)sg * ql.seg + (ql.seg - 1u - e);
     const uint32_t row = __builtin_amdgcn_readfirstlane(qp->row);
     const float* x = X + (size_t)row * dp;
     double best = 0.0;
@@ -763,6 +743,7 @@ __global__ __launch_bounds__(256) void k_fullscan(const float* __restrict__ X, i
       }
     }
     if (lane == 0) labels[row] = (bj == 0x7fffffff) ? 0 : bj;  // all-NaN distances: np.argmin -> 0
+   }
   }
 }
 

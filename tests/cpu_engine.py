@@ -1,0 +1,101 @@
+"""TEST-ONLY engine: the HipEngine interface computed on the CPU by the oracle.
+
+Used by the ``-m "not gpu"`` tests to exercise the product's host logic
+(KMeans driver, data placement, takeSample policy, empty-cluster repair,
+logging, the multi-rank all-reduce path over ``gloo``) without a GPU.  It is
+injected through ``KMeans._engine_factory``; the product never imports it.
+Arithmetic mirrors the device path: float32 rows, float64 statistics,
+closed-form SSE.
+"""
+import numpy as np
+
+from oracle import kmeans_oracle as orc
+
+
+class _Status:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+class OracleEngine:
+    def __init__(self, comm):
+        self.distributed = comm.world > 1
+        self.n = self.d = self.k = 0
+        self.mu = None
+        self.A = 0.0
+        self._stats_t = None
+
+    # data -------------------------------------------------------------------
+    def load_host(self, rows):
+        self.X = np.asarray(rows, dtype=np.float32).astype(np.float64)
+        self.n, self.d = self.X.shape if self.X.ndim == 2 else (0, 0)
+        return self.n
+
+    def sum_x(self):
+        return self.X.sum(axis=0) if self.n else np.zeros(self.d)
+
+    def sq_dev(self, mu):
+        self.mu = np.asarray(mu, dtype=np.float64)
+        return float(((self.X - self.mu) ** 2).sum()) if self.n else 0.0
+
+    def set_sse_base(self, v):
+        self.A = float(v)
+
+    # iteration --------------------------------------------------------------------
+    def set_centroids(self, C):
+        self.cur = np.array(C, dtype=np.float64)
+        self.k = len(self.cur)
+        self.new = self.cur.copy()
+
+    def get_centroids(self, which=0):
+        return (self.new if which else self.cur).copy()
+
+    def assign_stats(self):
+        import torch
+        S = np.zeros((self.k, self.d + 1))
+        if self.n:
+            self._labels = orc.assign(self.X, self.cur)[0]
+            np.add.at(S[:, :self.d], self._labels, self.X)
+            np.add.at(S[:, self.d], self._labels, 1.0)
+        else:
+            self._labels = np.zeros(0, dtype=np.int64)
+        self._stats_t = torch.from_numpy(S.ravel().copy())
+
+    def run_collective(self, fn):
+        fn(self._stats_t)
+
+    def update(self):
+        S = self._stats_t.numpy().reshape(self.k, self.d + 1)
+        cnt = S[:, self.d]
+        old = self.cur
+        new = np.where(cnt[:, None] > 0, S[:, :self.d] / np.where(cnt > 0, cnt, 1)[:, None], old)
+        self.new = new
+        shift = np.sqrt(((new - old) ** 2).sum(axis=1))
+        cmu = old - self.mu
+        t = np.where(cnt > 0, -2.0 * (cmu * (S[:, :self.d] - cnt[:, None] * self.mu)).sum(1)
+                     + cnt * (cmu ** 2).sum(1), 0.0)
+        st = _Status(sse=self.A + float(t.sum()), max_shift=float(shift.max()), n_empty=int((cnt == 0).sum()),
+                     nonfinite=int(not np.all(np.isfinite(new))), q_rerank=0, q_full=0)
+        return st, cnt.astype(np.int64)
+
+    def replace_rows(self, ids, rows):
+        self.new[np.asarray(ids)] = np.asarray(rows).reshape(len(ids), self.d)
+
+    def commit(self):
+        self.cur = self.new.copy()
+
+    def gather_rows(self, idx):
+        return self.X[np.asarray(idx, dtype=np.int64)]
+
+    def predict(self):
+        return orc.assign(self.X, self.cur)[0].astype(np.int32) if self.n else np.zeros(0, np.int32)
+
+    def labels(self):
+        return self._labels.astype(np.int32)
+
+    def info(self):
+        return {"n": self.n, "d": self.d, "k": self.k, "path": 0}
+
+
+def factory(comm):
+    return OracleEngine(comm)

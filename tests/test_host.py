@@ -1,0 +1,203 @@
+"""CPU tests of the host side: C-ABI library loads and exports the header's
+symbols, the takeSample policy, data placement, the KMeans driver (through a
+test-only oracle engine) against the reference's golden vectors, and the
+multi-rank path over gloo (world size 2)."""
+import contextlib
+import io
+import os
+import re
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle import kmeans_oracle as orc
+
+HEADER = os.path.join(ROOT, "include", "kmeans_amd.h")
+
+
+def _ka():
+    import kmeans_amd
+    return kmeans_amd
+
+
+# --------------------------------------------------------------------- C-ABI
+def test_library_exports_every_header_symbol():
+    from kmeans_amd import _lib
+    text = open(HEADER).read()
+    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(km_\w+)\s*\(", text, re.M))
+    assert declared, "no declarations parsed"
+    lib = _lib.load()
+    missing = [s for s in declared if not hasattr(lib, s)]
+    assert not missing, missing
+    assert declared == set(_lib.exported_symbols()), declared ^ set(_lib.exported_symbols())
+    assert lib.km_abi_version() == 1
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    ka = _ka()
+    with pytest.raises(RuntimeError):
+        ka.KMeans(k=2).fit(np.random.default_rng(0).standard_normal((100, 4)))
+
+
+# ------------------------------------------------------------------ sampling
+@pytest.mark.parametrize("sizes,num,seed", [
+    ([1000], 3, 42), ([250, 250, 250, 250], 6, 42), ([333, 333, 334], 5, 1700000000),
+    ([40000, 40000], 256, 6), ([70000], 10, 123), ([5], 6, 42), ([0, 7, 0], 3, 9),
+    ([100000, 1, 50000], 17, 2 ** 40 + 5),
+])
+def test_take_sample_matches_oracle_restatement(sizes, num, seed):
+    from kmeans_amd import sampling
+    assert sampling.take_sample(sizes, num, seed) == orc.take_sample_indices(sizes, num, seed)
+
+
+def test_vectorised_sampler_equals_python_sampler():
+    from kmeans_amd import sampling
+    sizes = [70001, 30000]
+    for seed in (0, 1, 42, 99991):
+        frac = sampling._fraction(50, sum(sizes))
+        assert sampling._bernoulli_pass(sizes, frac, seed) == sampling._bernoulli_pass_py(sizes, frac, seed)
+
+
+# ----------------------------------------------------------------- placement
+class FakeComm:
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+
+
+def test_placement_partitions_and_order():
+    ka = _ka()
+    from kmeans_amd.dataset import place
+    X = np.arange(1000 * 3, dtype=np.float64).reshape(1000, 3)
+    rdd = ka.LocalContext().parallelize(X, 5)
+    pls = [place(rdd, FakeComm(r, 2)) for r in range(2)]
+    assert pls[0].global_sizes == [200] * 5
+    assert [p.n_local for p in pls] == [400, 600]
+    np.testing.assert_array_equal(np.concatenate([p.local_rows for p in pls]), X)
+    assert pls[1].row0 == 400
+    np.testing.assert_array_equal(pls[1].host_rows([0, 999, 401]), X[[0, 999, 401]])
+    # a bare array is one takeSample partition, cut into row blocks per rank
+    pa = [place(X, FakeComm(r, 3)) for r in range(3)]
+    assert pa[0].global_sizes == [1000]
+    np.testing.assert_array_equal(np.concatenate([p.local_rows for p in pa]), X)
+    # device blobs: row split only
+    pb = place(ka.DeviceBlobs(n=10, d=4, n_centers=2), FakeComm(1, 3))
+    assert (pb.row0, pb.n_local, pb.global_sizes) == (3, 3, [3, 3, 4])
+
+
+def test_parallelize_slices_like_pyspark():
+    ka = _ka()
+    rdd = ka.LocalContext().parallelize(list(range(10)), 3)
+    assert [len(p) for p in rdd._parts] == [3, 3, 4]
+    assert rdd.collect() == list(range(10))
+    assert rdd.getNumPartitions() == 3
+
+
+def test_constructor_validation_messages():
+    ka = _ka()
+    for kw, msg in [({"k": 0}, "k must be positive, got 0"), ({"max_iter": 0}, "max_iter must be positive, got 0"),
+                    ({"tolerance": 0}, "tolerance must be positive, got 0"),
+                    ({"k": -2}, "k must be positive, got -2")]:
+        with pytest.raises(ValueError, match=re.escape(msg)):
+            ka.KMeans(**kw)
+    km = ka.KMeans(5, 10, 1e-3, 7, True)  # positional order of the reference (L37-38)
+    assert (km.k, km.max_iter, km.tolerance, km.seed, km.compute_sse) == (5, 10, 1e-3, 7, True)
+    assert km.centroids is None and km.sse_history == [] and km.iterations_run == 0
+
+
+# ----------------------------------------------- driver through the CPU engine
+@pytest.fixture
+def cpu_engine():
+    ka = _ka()
+    import cpu_engine as ce
+    old = ka.KMeans._engine_factory
+    ka.KMeans._engine_factory = staticmethod(ce.factory)
+    yield
+    ka.KMeans._engine_factory = old
+
+
+def _fit(g, inject=True):
+    ka = _ka()
+    init = g["init"]
+
+    class Pinned(ka.KMeans):
+        def _initialize_centroids(self, run):
+            return init.copy() if inject else super()._initialize_centroids(run)
+
+        def _empty_seed(self):
+            return int(g["time_seed"])
+
+    sc = ka.LocalContext()
+    rdd = sc.parallelize(g["X"], int(g["slices"]))
+    km = Pinned(k=int(g["k"]), max_iter=int(g["max_iter"]), tolerance=float(g["tol"]), seed=int(g["seed"]),
+                compute_sse=bool(g["sse"]))
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        km.fit(rdd, sc)
+    return km, buf.getvalue(), np.array(km.predict(rdd, sc).collect())
+
+
+@pytest.mark.parametrize("name", ["test_a", "test_d", "empty", "ties", "test_c"])
+def test_driver_reproduces_reference_with_cpu_engine(golden, cpu_engine, name):
+    from test_gpu_parity import assert_logs_match
+    g = golden(name)
+    km, out, labels = _fit(g, inject=(name in ("empty", "ties")))
+    np.testing.assert_allclose(km.centroids, g["centroids"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(km.sse_history, g["sse_history"], rtol=1e-9)
+    assert_logs_match(out, g["stdout"])
+    np.testing.assert_array_equal(labels, g["labels"])
+
+
+# ------------------------------------------------------ multi-rank over gloo
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, name, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import kmeans_amd as ka
+        import cpu_engine as ce
+        from conftest import load_golden
+        ka.KMeans._engine_factory = staticmethod(ce.factory)
+        g = load_golden(name)
+        km, out, labels = _fit(g, inject=(name in ("empty", "ties")))
+        q.put((rank, km.centroids, km.sse_history, labels, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["test_a", "test_d", "empty"])
+def test_two_ranks_gloo_match_single_rank(golden, name):
+    import torch.multiprocessing as mp
+    g = golden(name)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, name, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, C, sse, labels, out in res:
+        np.testing.assert_allclose(C, g["centroids"], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(sse, g["sse_history"], rtol=1e-9)
+        np.testing.assert_array_equal(labels, g["labels"])
+    assert res[0][4] and not res[1][4]  # only rank 0 logs, like the single driver
