@@ -39,23 +39,29 @@ struct Geometry {
   int32_t d;    // features
   int32_t dp;   // padded row stride of X (floats), multiple of 16
   int32_t k;    // clusters
-  int32_t kp;   // padded cluster count (multiple of 32)
+  int32_t kp;   // padded cluster count (multiple of 64)
 };
 
 // ---- launchers (km_kernels.hip) -------------------------------------------
-hipError_t launch_prep_centroids(const double* C64, const Geometry& g, float* C32, __bf16* Chi,
-                                 __bf16* Clo, float* cn2, float* cmax, double* C64T, hipStream_t s);
+hipError_t launch_prep_centroids(const double* C64, const Geometry& g, float* C32, float* cn2, float* cmax,
+                                 float* cabs, double* C64T, hipStream_t s);
+// fp16 hi/lo split of -2*c*s and ||c||^2 s^2 for the MFMA screen (s from the
+// data and centroid abs maxima)
+hipError_t launch_prep_split(const float* C32, const Geometry& g, const float* cn2, const float* xabs,
+                             const float* cabs, _Float16* Chi, _Float16* Clo, float* cn2s, hipStream_t s);
+hipError_t launch_absmax(const float* X, int64_t nfloats, float* out, hipStream_t s);
 // Small k*d path: direct-form fp32 screening, in-thread exact re-rank,
 // optional fused statistics (LDS float64 table, replicated per lane).
 hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C32, const double* C64,
                                const float* cmax, int32_t* labels, double* stats, int fuse_stats,
                                int n_cu, hipStream_t s);
 bool small_path_ok(const Geometry& g);
-// MFMA path: bf16x3 screening on v_mfma_f32_32x32x16_bf16, top-3 keys,
-// ambiguous points queued for k_resolve.
-hipError_t launch_assign_mfma(const float* X, const Geometry& g, const __bf16* Chi, const __bf16* Clo,
-                              const float* cn2, const float* cmax, int32_t* labels, QEntry* queue,
-                              uint32_t* qcount, int n_cu, QLayout* ql, hipStream_t s);
+// MFMA path: fp16x3 screening on v_mfma_f32_32x32x16_f16, top-3 keys,
+// ambiguous points queued for the exact resolvers.
+hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16* Chi, const _Float16* Clo,
+                              const float* cn2s, const float* cmax, const float* xabs, const float* cabs,
+                              int32_t* labels, QEntry* queue, uint32_t* qcount, int n_cu, QLayout* ql,
+                              hipStream_t s);
 // queue capacity (entries) and per-wave counter words needed for n rows
 size_t queue_capacity(int64_t n, int n_cu);
 size_t qcount_words(int n_cu);

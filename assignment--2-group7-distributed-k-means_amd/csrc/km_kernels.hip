@@ -15,11 +15,9 @@
 
 namespace km {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 static constexpr float U24 = 5.9604644775390625e-08f;  // 2^-24, fp32 unit roundoff
-static constexpr float U16 = 1.52587890625e-05f;       // 2^-16, bf16x2 split residual
 
 __host__ __device__ inline int ceil_log2(int v) {
   int b = 0;
@@ -93,25 +91,28 @@ __device__ inline float wave_sum_f(float v) {
 // Padded rows (k <= j < kp) are zero with ||c||^2 = 1e30 (never selected).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_prep_centroids(const double* __restrict__ C64, int k, int d, int dp,
-                                                       float* __restrict__ C32, __bf16* __restrict__ Chi,
-                                                       __bf16* __restrict__ Clo, float* __restrict__ cn2,
-                                                       float* __restrict__ cmax, double* __restrict__ C64T) {
+                                                       float* __restrict__ C32, float* __restrict__ cn2,
+                                                       float* __restrict__ cmax, float* __restrict__ cabs,
+                                                       double* __restrict__ C64T) {
   const int j = blockIdx.x;
   const int lane = threadIdx.x;
   double nn = 0.0;
+  float am = 0.0f;
   for (int f = lane; f < dp; f += 64) {
     const double c = (j < k && f < d) ? C64[(size_t)j * d + f] : 0.0;
     if (j < k && f < d) C64T[(size_t)f * k + j] = c;
     nn = fma(c, c, nn);
     const float c32 = (float)c;
     C32[(size_t)j * dp + f] = c32;
-    const float m2 = -2.0f * c32;
-    const __bf16 hi = (__bf16)m2;
-    const __bf16 lo = (__bf16)(m2 - (float)hi);
-    Chi[(size_t)j * dp + f] = hi;
-    Clo[(size_t)j * dp + f] = lo;
+    am = (fabsf(c32) > am || c32 != c32) ? fabsf(c32) : am;
   }
   nn = wave_sum(nn);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float t = __shfl_xor(am, o);
+    am = (t > am || t != t) ? t : am;
+  }
+  if (lane == 0 && j < k) atomicMax((unsigned int*)cabs, __float_as_uint(am));
   if (lane == 0) {
     cn2[j] = (j < k) ? (float)nn : 1e30f;
     if (j < k) {
@@ -121,11 +122,13 @@ __global__ __launch_bounds__(64) void k_prep_centroids(const double* __restrict_
   }
 }
 
-hipError_t launch_prep_centroids(const double* C64, const Geometry& g, float* C32, __bf16* Chi, __bf16* Clo,
-                                 float* cn2, float* cmax, double* C64T, hipStream_t s) {
+hipError_t launch_prep_centroids(const double* C64, const Geometry& g, float* C32, float* cn2, float* cmax,
+                                 float* cabs, double* C64T, hipStream_t s) {
   hipError_t e = hipMemsetAsync(cmax, 0, sizeof(float), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_prep_centroids, dim3(g.kp), dim3(64), 0, s, C64, g.k, g.d, g.dp, C32, Chi, Clo, cn2, cmax, C64T);
+  e = hipMemsetAsync(cabs, 0, sizeof(float), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_prep_centroids, dim3(g.kp), dim3(64), 0, s, C64, g.k, g.d, g.dp, C32, cn2, cmax, cabs, C64T);
   return hipGetLastError();
 }
 
@@ -284,89 +287,128 @@ hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C
 // ---------------------------------------------------------------------------
 // MFMA screening path (c3/c4/c5 shapes).
 //
-// scores S[j][p] = ||c_j||^2 - 2 c_j.x_p on v_mfma_f32_32x32x16_bf16 with a
-// bf16x3 split (-2c = ch + cl, x = xh + xl; ch*xh + ch*xl + cl*xh), A operand
-// = 32 centroids from LDS, B operand = 32 points held in registers, the
-// accumulator initialised with ||c||^2.  C/D layout: column (point) on the
-// lane, rows (centroids) in registers, so each lane keeps a running top-3 of
-// (score | centroid index in the low mantissa bits) with min/med3.  The two
-// lane halves hold disjoint centroid rows and are merged at the end.
+// Scores S[j][p] = ||c_j||^2 - 2 c_j.x_p on v_mfma_f32_32x32x16_f16 with an
+// fp16x3 split: with a power-of-two scale s (data and centroids into
+// |.| < 2^14), -2cs = ch + cl and xs = xh + xl (fp16 halves, 22 bits), and
+// S s^2 ~ ||cs||^2 + ch.xl + cl.xh + ch.xh accumulated in fp32.  A operand =
+// 32 centroids (LDS), B operand = 32 points (registers), accumulator
+// initialised with ||c||^2 s^2.  C/D layout: column (point) on the lane,
+// centroid rows in registers; each lane keeps four independent running
+// top-3 chains of (score | j>>2 in the low mantissa bits) with v_med3, the
+// chain id carrying j & 3.  Blocks of 32 centroids are software-pipelined in
+// pairs so one block's key updates overlap the next block's MFMAs.
 // ---------------------------------------------------------------------------
 static constexpr int MFMA_LDS_LARGE = 160 * 1024;  // LDS per CU
 
-template <int NS>
-__device__ __forceinline__ int phys_chunk(int c, int row) {
-  constexpr int C = 2 * NS;  // 16-byte chunks per bf16 row
-  if constexpr ((C & (C - 1)) == 0) {
-    return c ^ ((row >> 1) & (C - 1));
-  } else {
-    return c;
-  }
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// power-of-two scale: max(|x|, |c|) * s < 2^14 (so |-2cs| < 2^15 < 65504);
+// 1 for non-finite or all-zero data (the keys then force the exact path)
+__device__ __forceinline__ float mfma_scale(float xabs, float cabs) {
+  const float m = fmaxf(xabs, cabs);
+  if (!(m > 0.0f) || !(m < 3.0e38f)) return 1.0f;
+  int e;
+  (void)frexpf(m, &e);  // m < 2^e
+  return ldexpf(1.0f, 14 - e);
 }
 
-// Raw fp32 B-operand data of one 32-point tile: lane (r, h) holds features
-// [16s + 8h, 16s + 8h + 8) of point r for every K-step s.
-template <int NS>
-__device__ __forceinline__ void load_tile(const float* __restrict__ X, int64_t n, int64_t tile, int r, int h,
-                                          float4 (&xr)[2 * NS]) {
-  const int64_t row = tile * 32 + r;
-  const int64_t rl = row < n ? row : (n - 1);
-  const float* p = X + rl * (16 * NS) + 8 * h;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    xr[2 * s] = *reinterpret_cast<const float4*>(p + 16 * s);
-    xr[2 * s + 1] = *reinterpret_cast<const float4*>(p + 16 * s + 4);
+__global__ __launch_bounds__(64) void k_prep_split(const float* __restrict__ C32, int kp, int dp,
+                                                   const float* __restrict__ cn2, const float* __restrict__ xabs,
+                                                   const float* __restrict__ cabs, _Float16* __restrict__ Chi,
+                                                   _Float16* __restrict__ Clo, float* __restrict__ cn2s, int k) {
+  const int j = blockIdx.x;
+  const float s = mfma_scale(*xabs, *cabs);
+  for (int f = threadIdx.x; f < dp; f += 64) {
+    const float m2 = -2.0f * C32[(size_t)j * dp + f] * s;
+    const _Float16 hi = (_Float16)m2;
+    Chi[(size_t)j * dp + f] = hi;
+    Clo[(size_t)j * dp + f] = (_Float16)(m2 - (float)hi);
   }
+  if (threadIdx.x == 0) cn2s[j] = (j < k) ? cn2[j] * s * s : 1e30f;
 }
 
-// 8-wave workgroups; up to d = 64 two of them share a CU (4 waves per SIMD,
-// <= 128 VGPRs), wider rows get one (2 per SIMD).
+// top-3 insert carrying the index of the two best (a candidate equal to a
+// kept key does not displace it)
+__device__ __forceinline__ void top3p_insert(float& k1, float& k2, float& k3, uint32_t& p1, uint32_t& p2, float v,
+                                             uint32_t pv) {
+  const bool lt1 = v < k1, lt2 = v < k2, lt3 = v < k3;
+  const float n3 = lt2 ? k2 : (lt3 ? v : k3);
+  const float n2 = lt1 ? k1 : (lt2 ? v : k2);
+  const uint32_t q2 = lt1 ? p1 : (lt2 ? pv : p2);
+  k1 = lt1 ? v : k1;
+  p1 = lt1 ? pv : p1;
+  k2 = n2;
+  p2 = q2;
+  k3 = n3;
+}
+
 template <int NS, int WAVES>
 constexpr int mfma_min_waves() {
-  return WAVES == 4 ? 1 : (NS <= 4 ? 4 : 2);
+  return WAVES == 4 ? 1 : (WAVES == 12 ? 3 : (NS <= 4 ? 4 : 2));
 }
 
-template <int NS, int WAVES, bool PF>
-__global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_assign_mfma(const float* __restrict__ X, int64_t n, int k,
-                                                              int kp, const __bf16* __restrict__ Chi,
-                                                              const __bf16* __restrict__ Clo,
-                                                              const float* __restrict__ cn2,
-                                                              const float* __restrict__ cmaxp,
-                                                              int32_t* __restrict__ labels, QEntry* __restrict__ queue,
-                                                              uint32_t* __restrict__ qcount, int KC, uint32_t seg) {
+struct MfmaArgs {
+  const float* X;
+  int64_t n;
+  int k, kp, KC;
+  uint32_t seg;
+  const _Float16* Chi;
+  const _Float16* Clo;
+  const float* cn2s;
+  const float* cmax;
+  const float* xabs;
+  const float* cabs;
+  int32_t* labels;
+  QEntry* queue;
+  uint32_t* qcount;
+};
+
+// LDS image of a centroid chunk: for block b (32 centroids) and K-step t the
+// A fragment is one contiguous 1 KiB piece, lane l at byte 16*l (rows
+// 32b + (l&31), features 16t + 8(l>>5) .. +8): lane-linear, bank-conflict
+// free, and every read of a block is base + immediate offset.
+// ABL (diagnostic builds only, never selected by default): 1 = no key
+// updates, 2 = no MFMAs (labels are then wrong; timing only)
+template <int NS, int WAVES, int ABL = 0>
+__global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_assign_mfma(MfmaArgs A) {
   constexpr int DP = 16 * NS;
-  constexpr int ROWB = DP * 2;  // bytes per bf16 row
+  constexpr int BLKB = NS * 1024;  // bytes of one block's fragments (one of hi / lo)
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int KC = A.KC;
+  const size_t himg = (size_t)(KC / 32) * BLKB;
   char* sHi = smem;
-  char* sLo = smem + (size_t)KC * ROWB;
-  float* sCn = reinterpret_cast<float*>(smem + 2 * (size_t)KC * ROWB);
+  char* sLo = smem + himg;
+  float* sCn = reinterpret_cast<float*>(smem + 2 * himg);
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int r = lane & 31;
   const int h = lane >> 5;
-  const int b = ceil_log2(kp);
-  const uint32_t mask = (1u << b) - 1u;
-  const float cm = *cmaxp;
-  // key truncation (index bits in the low mantissa), relative
-  const float rho = __builtin_ldexpf(1.0f, b - 23) * 1.01f;
+  const int kp = A.kp;
+  const int64_t n = A.n;
+  const int b = ceil_log2(kp);  // kp is a multiple of 64: b >= 6
+  const uint32_t maskq = (1u << (b - 2)) - 1u;
+  const float s = mfma_scale(*A.xabs, *A.cabs);
+  const float cm = *A.cmax * s;
+  const float rho = __builtin_ldexpf(1.0f, b - 2 - 23) * 1.01f;  // key truncation (relative)
   const int nchunks = (kp + KC - 1) / KC;
   const int64_t ntiles = (n + 31) / 32;
   const int64_t nwt = (ntiles + WAVES - 1) / WAVES;
 
   auto stage = [&](int ch) {
     const int kc = min(KC, kp - ch * KC);
-    const int nc = kc * 2 * NS;
-    const char* gh = reinterpret_cast<const char*>(Chi + (size_t)ch * KC * DP);
-    const char* gl = reinterpret_cast<const char*>(Clo + (size_t)ch * KC * DP);
-    for (int id = threadIdx.x; id < nc; id += WAVES * 64) {
-      const int row = id / (2 * NS);
-      const int c = id % (2 * NS);
-      const size_t dst = (size_t)row * ROWB + (size_t)phys_chunk<NS>(c, row) * 16;
-      *reinterpret_cast<uint4*>(sHi + dst) = *reinterpret_cast<const uint4*>(gh + (size_t)id * 16);
-      *reinterpret_cast<uint4*>(sLo + dst) = *reinterpret_cast<const uint4*>(gl + (size_t)id * 16);
+    const int npieces = (kc / 32) * NS * 64;  // 16-byte pieces per image
+    const char* gh = reinterpret_cast<const char*>(A.Chi + (size_t)ch * KC * DP);
+    const char* gl = reinterpret_cast<const char*>(A.Clo + (size_t)ch * KC * DP);
+    for (int id = threadIdx.x; id < npieces; id += WAVES * 64) {
+      const int l = id & 63;
+      const int bt = id >> 6;  // blk * NS + t
+      const int blk = bt / NS, t = bt - blk * NS;
+      const size_t src = ((size_t)(blk * 32 + (l & 31)) * DP + 16 * t + 8 * (l >> 5)) * 2;
+      *reinterpret_cast<uint4*>(sHi + (size_t)id * 16) = *reinterpret_cast<const uint4*>(gh + src);
+      *reinterpret_cast<uint4*>(sLo + (size_t)id * 16) = *reinterpret_cast<const uint4*>(gl + src);
     }
-    for (int id = threadIdx.x; id < kc; id += WAVES * 64) sCn[id] = cn2[(size_t)ch * KC + id];
+    for (int id = threadIdx.x; id < kc; id += WAVES * 64) sCn[id] = A.cn2s[(size_t)ch * KC + id];
   };
 
   if (nchunks == 1) {
@@ -377,130 +419,176 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
   // per-wave queue segment: no global counter (one hot address would
   // serialise every wave at the memory side)
   const uint32_t gw = blockIdx.x * WAVES + wave;
-  QEntry* wq = queue + (size_t)gw * seg;
+  QEntry* wq = A.queue + (size_t)gw * A.seg;
   uint32_t qn = 0, qf = 0;
+  const char* laneHi = sHi + lane * 16;
+  const char* laneLo = sLo + lane * 16;
+  const float* laneCn = sCn + 4 * h;
 
-  float4 xr[2 * NS];
-  int64_t wt = blockIdx.x;
-  if (PF && wt < nwt) load_tile<NS>(X, n, wt * WAVES + wave, r, h, xr);
-  for (; wt < nwt; wt += gridDim.x) {
+  for (int64_t wt = blockIdx.x; wt < nwt; wt += gridDim.x) {
     const int64_t tile = wt * WAVES + wave;
     if (nchunks == 1 && tile >= ntiles) break;  // no barriers below in this mode
-    if (!PF) load_tile<NS>(X, n, tile, r, h, xr);
     const int64_t row = tile * 32 + r;
     const bool valid = row < n;
+    const float* xr = A.X + (valid ? row : (n - 1)) * DP + 8 * h;
 
-    bf16x8 bh[NS], bl[NS];
+    // B operand: lane (r, h) holds features [16t + 8h, 16t + 8h + 8) of point r
+    f16x8 bh[NS], bl[NS];
     float xx = 0.0f;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const float4 v0 = xr[2 * s];
-      const float4 v1 = xr[2 * s + 1];
+    for (int t = 0; t < NS; ++t) {
+      const float4 v0 = *reinterpret_cast<const float4*>(xr + 16 * t);
+      const float4 v1 = *reinterpret_cast<const float4*>(xr + 16 * t + 4);
       const float xv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const __bf16 hi = (__bf16)xv[e];
-        bh[s][e] = hi;
-        bl[s][e] = (__bf16)(xv[e] - (float)hi);
-        xx = fmaf(xv[e], xv[e], xx);
+        const float xs = xv[e] * s;
+        const _Float16 hi = (_Float16)xs;
+        bh[t][e] = hi;
+        bl[t][e] = (_Float16)(xs - (float)hi);
+        xx = fmaf(xs, xs, xx);
       }
     }
     xx += __shfl_xor(xx, 32);
-    // software pipelining: the next tile's rows are in flight during this tile's MFMAs
-    if (PF && wt + gridDim.x < nwt) load_tile<NS>(X, n, (wt + gridDim.x) * WAVES + wave, r, h, xr);
 
-    // Four independent top-3 chains (ILP).  Chain c takes the accumulator
-    // registers reg = c, c+4, c+8, c+12, whose centroid index j has j & 3 == c,
-    // so a chain key stores only j >> 2 in its low mantissa bits (one v_bfi per
-    // score); the chain id is put back when the chains are merged.
-    const uint32_t maskq = mask >> 2;
     float a1[4], a2[4], a3[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) a1[c] = a2[c] = a3[c] = FLT_MAX;
+
+    auto init_acc = [&](int blk) {
+      f32x16 acc;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 cv = *reinterpret_cast<const float4*>(laneCn + blk * 32 + 8 * g4);
+        acc[4 * g4 + 0] = cv.x;
+        acc[4 * g4 + 1] = cv.y;
+        acc[4 * g4 + 2] = cv.z;
+        acc[4 * g4 + 3] = cv.w;
+      }
+      return acc;
+    };
+    struct Frag {
+      f16x8 hi, lo;
+    };
+    auto load_frag = [&](int blk, int t) {
+      const size_t off = (size_t)blk * BLKB + (size_t)t * 1024;
+      Frag f;
+      f.hi = *reinterpret_cast<const f16x8*>(laneHi + off);
+      f.lo = *reinterpret_cast<const f16x8*>(laneLo + off);
+      return f;
+    };
+    auto mfma3 = [&](f32x16 acc, const Frag& f, int t) {
+      if constexpr (ABL == 2) {
+        acc[t] += (float)f.hi[0] + (float)f.lo[1] + (float)bl[t][2] + (float)bh[t][3];
+        return acc;
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.hi, bl[t], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.lo, bh[t], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.hi, bh[t], acc, 0, 0, 0);
+      return acc;
+    };
+    // register reg of block blk holds centroid j = 32*blk + 4h + (reg&3) + 8*(reg>>2);
+    // chain reg&3 stores j >> 2 = (8*blk + h) | 2*(reg>>2) in the key
+    uint32_t jg[4];
+    auto set_jg = [&](uint32_t jq) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        jg[g] = jq | (uint32_t)(2 * g);
+        asm volatile("" : "+v"(jg[g]));  // keep it a register: one v_and_or per key
+      }
+    };
+    auto key_update = [&](const f32x16& acc, int reg) {
+      if constexpr (ABL == 1) {
+        if (reg == 0) a1[0] = fminf(a1[0], acc[0] + acc[15]);
+        asm volatile("" ::"v"(acc[reg]));
+        return;
+      }
+      const float key = __uint_as_float((__float_as_uint(acc[reg]) & ~maskq) | jg[reg >> 2]);
+      top3_insert(a1[reg & 3], a2[reg & 3], a3[reg & 3], key);
+    };
+    // MFMAs of block `blk` into `cur` while the 16 key updates of the
+    // previous block (`prev`, index words already in jg) fill the gaps.  A
+    // fragments are prefetched one K-step ahead (into the next block at the
+    // last step) so no MFMA waits on its own LDS read.
+    Frag fr = load_frag(0, 0);
+    auto overlapped = [&](f32x16& cur, int blk, int nblk, const f32x16& prev) {
+      cur = init_acc(blk);
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+        const Frag nx = (t + 1 < NS) ? load_frag(blk, t + 1) : load_frag(blk + 1 < nblk ? blk + 1 : blk, 0);
+        cur = mfma3(cur, fr, t);
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr)
+          if (rr * NS / 16 == t) key_update(prev, rr);
+        fr = nx;
+      }
+    };
+
     for (int ch = 0; ch < nchunks; ++ch) {
       if (nchunks > 1) {
         __syncthreads();
         stage(ch);
         __syncthreads();
+        fr = load_frag(0, 0);
       }
-      const int kc = min(KC, kp - ch * KC);
-      for (int blk = 0; blk < kc / 32; ++blk) {
-        const int crow = blk * 32 + r;
-        bf16x8 ah[NS], al[NS];
+      const int nb = min(KC, kp - ch * KC) / 32;  // even: kp and KC are multiples of 64
+      const uint32_t jq0 = (uint32_t)((ch * KC) >> 2) + (uint32_t)h;
+      f32x16 accA = init_acc(0), accB;
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          const size_t off = (size_t)crow * ROWB + (size_t)phys_chunk<NS>(2 * s + h, crow) * 16;
-          ah[s] = *reinterpret_cast<const bf16x8*>(sHi + off);
-          al[s] = *reinterpret_cast<const bf16x8*>(sLo + off);
-        }
-        f32x16 acc;
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const float4 cv = *reinterpret_cast<const float4*>(sCn + blk * 32 + 8 * g4 + 4 * h);
-          acc[4 * g4 + 0] = cv.x;
-          acc[4 * g4 + 1] = cv.y;
-          acc[4 * g4 + 2] = cv.z;
-          acc[4 * g4 + 3] = cv.w;
-        }
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bl[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s], bh[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bh[s], acc, 0, 0, 0);
-        }
-        // j = 32*blk + 4h + (reg & 3) + 8*(reg >> 2)  =>  j >> 2 = (8*blk + h) | 2*(reg >> 2)
-        const uint32_t jq = (uint32_t)((ch * KC + blk * 32) >> 2) + (uint32_t)h;
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          const uint32_t jf = jq | (uint32_t)(2 * (reg >> 2));
-          const float key = __uint_as_float((__float_as_uint(acc[reg]) & ~maskq) | jf);
-          top3_insert(a1[reg & 3], a2[reg & 3], a3[reg & 3], key);
-        }
+      for (int t = 0; t < NS; ++t) {
+        const Frag nx = (t + 1 < NS) ? load_frag(0, t + 1) : load_frag(1, 0);
+        accA = mfma3(accA, fr, t);
+        fr = nx;
       }
+      int blk = 1;
+      for (; blk + 1 < nb; blk += 2) {
+        set_jg(jq0 + 8u * (uint32_t)(blk - 1));
+        overlapped(accB, blk, nb, accA);
+        set_jg(jq0 + 8u * (uint32_t)blk);
+        overlapped(accA, blk + 1, nb, accB);
+      }
+      set_jg(jq0 + 8u * (uint32_t)(blk - 1));
+      overlapped(accB, blk, nb, accA);
+      set_jg(jq0 + 8u * (uint32_t)blk);
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) key_update(accB, rr);
     }
     if (nchunks > 1 && tile >= ntiles) continue;
 
-    // chain keys -> full-index keys: j = (field << 2) | c
-    auto full_key = [&](float kk, uint32_t c) -> float {
-      const uint32_t u = __float_as_uint(kk);
-      return __uint_as_float((u & ~mask) | ((((u & maskq) << 2) | c) & mask));
-    };
-    float k1 = full_key(a1[0], 0), k2 = full_key(a2[0], 0), k3 = full_key(a3[0], 0);
+    // exact merge of the 4 chains, carrying full indices of the best two
+    float k1 = FLT_MAX, k2 = FLT_MAX, k3 = FLT_MAX;
+    uint32_t p1 = 0, p2 = 0;
 #pragma unroll
-    for (int c = 1; c < 4; ++c) {
-      top3_insert(k1, k2, k3, full_key(a1[c], (uint32_t)c));
-      top3_insert(k1, k2, k3, full_key(a2[c], (uint32_t)c));
-      top3_insert(k1, k2, k3, full_key(a3[c], (uint32_t)c));
+    for (int c = 0; c < 4; ++c) {
+      top3p_insert(k1, k2, k3, p1, p2, a1[c], ((__float_as_uint(a1[c]) & maskq) << 2) | (uint32_t)c);
+      top3p_insert(k1, k2, k3, p1, p2, a2[c], ((__float_as_uint(a2[c]) & maskq) << 2) | (uint32_t)c);
+      top3p_insert(k1, k2, k3, p1, p2, a3[c], 0u);  // a 3rd never enters the top two
     }
-    // merge the two lane halves (disjoint centroid rows of the same point)
-    {
-      const float p1 = __shfl_xor(k1, 32);
-      const float p2 = __shfl_xor(k2, 32);
-      const float p3 = __shfl_xor(k3, 32);
-      top3_insert(k1, k2, k3, p1);
-      top3_insert(k1, k2, k3, p2);
-      top3_insert(k1, k2, k3, p3);
+    {  // the two lane halves hold disjoint centroid rows of the same point
+      const float q1 = __shfl_xor(k1, 32), q2 = __shfl_xor(k2, 32), q3 = __shfl_xor(k3, 32);
+      const uint32_t r1 = __shfl_xor(p1, 32), r2 = __shfl_xor(p2, 32);
+      top3p_insert(k1, k2, k3, p1, p2, q1, r1);
+      top3p_insert(k1, k2, k3, p1, p2, q2, r2);
+      top3p_insert(k1, k2, k3, p1, p2, q3, 0u);
     }
-    // Rigorous bound on |K_j - (||x - c_j||^2 - ||x||^2)| (DESIGN.md "Exactness"):
-    //   bf16x3 split residuals + fp32 accumulation + fp32 rounding of ||c||^2
-    //   (B0), plus the key truncation rho*|K| (index bits).
+    // Rigorous bound on |K_j - s^2 (||x - c_j||^2 - ||x||^2)| (DESIGN.md
+    // "Exactness"): fp16x3 split residuals, fp64->fp32 rounding of c, fp32
+    // accumulation, ||c||^2 rounding, fp16 underflow (B0); plus the key
+    // truncation rho*|K|.  x1.5 safety.
     const float xn = sqrtf(xx) * 1.0001f;
-    const float B0 = 1.5f * ((6.5f * U16 + (float)(6 * DP + 8) * U24) * xn * cm +
-                             (float)(3 * DP + 4) * U24 * cm * cm + 4.0f * U24 * (xx + cm * cm + 2.0f * xn * cm));
-    // (2.5x on the far side: chain keys were selected at b-2 bits, re-keyed at b)
-    const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + 2.5f * fabsf(k3));
-    const float thr2 = 2.0f * B0 + rho * (fabsf(k1) + 2.5f * fabsf(k2));
-    const uint32_t i1 = __float_as_uint(k1) & mask;
-    const uint32_t i2 = __float_as_uint(k2) & mask;
-    // negated tests: a NaN (non-finite data) falls through to the full float64
+    const float B0 = 1.5f * ((6.5f * 2.384185791015625e-07f + 0.5f * U24 + (float)(6 * DP + 8) * U24) * xn * cm +
+                             (float)(3 * DP + 5) * U24 * cm * cm + U24 * sqrtf((float)DP) * (xn + 2.0f * cm));
+    const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k3));
+    const float thr2 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k2));
+    // negated tests: NaN (non-finite data) falls through to the full float64
     // scan, whose np.argmin semantics then pick the first index
     uint32_t kind = 0;
     if (!(k3 - k1 > thr3))
       kind = 2;
     else if (!(k2 - k1 > thr2))
       kind = 1;
-    int lab = (i1 < (uint32_t)k) ? (int)i1 : 0;
-    if (h == 0 && valid) labels[row] = lab;
+    const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
+    if (h == 0 && valid) A.labels[row] = lab;
     const bool enq = (h == 0) && valid && (kind != 0);
     const uint64_t m = __ballot(enq);
     if (m) {
@@ -512,11 +600,11 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
       if (enq) {
         QEntry q;
         q.row = (uint32_t)row;
-        q.i1 = i1;
-        q.i2 = i2;
+        q.i1 = p1;
+        q.i2 = p2;
         q.kind = kind;
         const uint32_t pos = (kind == 1) ? qn + (uint32_t)__popcll(m1 & below)
-                                         : seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
+                                         : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
         wq[pos] = q;
       }
       qn += (uint32_t)__popcll(m1);
@@ -524,25 +612,25 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
     }
   }
   if (lane == 0) {
-    qcount[2 * gw] = qn;
-    qcount[2 * gw + 1] = qf;
+    A.qcount[2 * gw] = qn;
+    A.qcount[2 * gw + 1] = qf;
   }
+}
+
+static int mfma_waves_env() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("KM_MFMA_WAVES");  // experiment knob: 12 (default) or 8
+    v = (e && e[0] == '8') ? 8 : 12;
+  }
+  return v;
 }
 
 static int mfma_kc(const Geometry& g, int* waves) {
   const size_t per = (size_t)g.dp * 4 + 4;
-  *waves = (g.dp >= 192) ? 4 : 8;
+  *waves = (g.dp >= 192) ? 4 : (g.dp <= 64 ? mfma_waves_env() : 8);
   if ((size_t)g.kp * per <= MFMA_LDS_LARGE) return g.kp;
-  return (int)((MFMA_LDS_LARGE / per) / 32 * 32);
-}
-
-static bool mfma_prefetch() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("KM_MFMA_PREFETCH");  // default off: with 4 waves/SIMD the other waves hide it
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v == 1;
+  return (int)((MFMA_LDS_LARGE / per) / 64 * 64);
 }
 
 // at most 2 workgroups x 8 waves per CU, each wave's segment rounded up to
@@ -553,42 +641,57 @@ size_t qcount_words(int n_cu) { return (size_t)2 * 16 * n_cu + 16; }
 bool mfma_path_ok(const Geometry& g) {
   switch (g.dp) {
     case 16: case 32: case 48: case 64: case 96: case 128: case 192: case 256:
-      return g.kp >= 32 && g.kp % 32 == 0 && g.kp <= (1 << 20);
+      return g.kp >= 64 && g.kp % 64 == 0 && g.kp <= (1 << 20);
     default:
       return false;
   }
 }
 
+hipError_t launch_prep_split(const float* C32, const Geometry& g, const float* cn2, const float* xabs,
+                             const float* cabs, _Float16* Chi, _Float16* Clo, float* cn2s, hipStream_t s) {
+  hipLaunchKernelGGL(k_prep_split, dim3(g.kp), dim3(64), 0, s, C32, g.kp, g.dp, cn2, xabs, cabs, Chi, Clo, cn2s,
+                     g.k);
+  return hipGetLastError();
+}
+
 template <int NS>
-static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, const float* X, const Geometry& g,
-                           const __bf16* Chi, const __bf16* Clo, const float* cn2, const float* cmax,
-                           int32_t* labels, QEntry* queue, uint32_t* qcount, int KC, uint32_t seg) {
-  if (waves == 4) {
-    hipLaunchKernelGGL((k_assign_mfma<NS, 4, true>), dim3(blocks), dim3(256), lds, s, X, g.n, g.k, g.kp, Chi, Clo,
-                       cn2, cmax, labels, queue, qcount, KC, seg);
-  } else if (mfma_prefetch()) {
-    hipLaunchKernelGGL((k_assign_mfma<NS, 8, true>), dim3(blocks), dim3(512), lds, s, X, g.n, g.k, g.kp, Chi, Clo,
-                       cn2, cmax, labels, queue, qcount, KC, seg);
+static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, const MfmaArgs& a) {
+  if constexpr (NS >= 12) {
+    hipLaunchKernelGGL((k_assign_mfma<NS, 4>), dim3(blocks), dim3(256), lds, s, a);
   } else {
-    hipLaunchKernelGGL((k_assign_mfma<NS, 8, false>), dim3(blocks), dim3(512), lds, s, X, g.n, g.k, g.kp, Chi, Clo,
-                       cn2, cmax, labels, queue, qcount, KC, seg);
+    if (waves == 4)
+      hipLaunchKernelGGL((k_assign_mfma<NS, 4>), dim3(blocks), dim3(256), lds, s, a);
+    else if (waves == 12)
+      hipLaunchKernelGGL((k_assign_mfma<NS, 12>), dim3(blocks), dim3(768), lds, s, a);
+    else
+      hipLaunchKernelGGL((k_assign_mfma<NS, 8>), dim3(blocks), dim3(512), lds, s, a);
+    if constexpr (NS == 4) {  // diagnostic ablations (KM_ABLATE=1|2), c3 shape only
+      static const char* e = getenv("KM_ABLATE");
+      if (e && (e[0] == '1' || e[0] == '2')) {
+        if (e[0] == '1')
+          hipLaunchKernelGGL((k_assign_mfma<NS, 12, 1>), dim3(blocks), dim3(768), lds, s, a);
+        else
+          hipLaunchKernelGGL((k_assign_mfma<NS, 12, 2>), dim3(blocks), dim3(768), lds, s, a);
+      }
+    }
   }
 }
 
-hipError_t launch_assign_mfma(const float* X, const Geometry& g, const __bf16* Chi, const __bf16* Clo,
-                              const float* cn2, const float* cmax, int32_t* labels, QEntry* queue,
-                              uint32_t* qcount, int n_cu, QLayout* ql, hipStream_t s) {
+hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16* Chi, const _Float16* Clo,
+                              const float* cn2s, const float* cmax, const float* xabs, const float* cabs,
+                              int32_t* labels, QEntry* queue, uint32_t* qcount, int n_cu, QLayout* ql,
+                              hipStream_t s) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
   int waves = 8;
   const int KC = mfma_kc(g, &waves);
-  if (KC < 32) return hipErrorInvalidValue;
+  if (KC < 64) return hipErrorInvalidValue;
   const size_t lds = 2 * (size_t)KC * g.dp * 2 + (size_t)KC * 4;
   const int64_t ntiles = (g.n + 31) / 32;
   const int64_t nwt = (ntiles + waves - 1) / waves;
   int per_cu = (int)(MFMA_LDS_LARGE / lds);
-  const int max_per_cu = (waves == 4) ? 1 : (g.dp <= 64 ? 2 : 1);
+  const int max_per_cu = (waves == 8 && g.dp <= 64) ? 2 : 1;
   if (per_cu > max_per_cu) per_cu = max_per_cu;
   if (per_cu < 1) per_cu = 1;
   int64_t blocks = (int64_t)n_cu * per_cu;
@@ -597,17 +700,41 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const __bf16* C
   const uint32_t seg = (uint32_t)(((nwt + nb - 1) / nb) * 32);
   ql->seg = seg;
   ql->nwaves = (uint32_t)(nb * waves);
+  MfmaArgs a{X, g.n, g.k, g.kp, KC, seg, Chi, Clo, cn2s, cmax, xabs, cabs, labels, queue, qcount};
   switch (g.dp / 16) {
-    case 1: launch_mfma_ns<1>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
-    case 2: launch_mfma_ns<2>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
-    case 3: launch_mfma_ns<3>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
-    case 4: launch_mfma_ns<4>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
-    case 6: launch_mfma_ns<6>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
-    case 8: launch_mfma_ns<8>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
-    case 12: launch_mfma_ns<12>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
-    case 16: launch_mfma_ns<16>(waves, nb, lds, s, X, g, Chi, Clo, cn2, cmax, labels, queue, qcount, KC, seg); break;
+    case 1: launch_mfma_ns<1>(waves, nb, lds, s, a); break;
+    case 2: launch_mfma_ns<2>(waves, nb, lds, s, a); break;
+    case 3: launch_mfma_ns<3>(waves, nb, lds, s, a); break;
+    case 4: launch_mfma_ns<4>(waves, nb, lds, s, a); break;
+    case 6: launch_mfma_ns<6>(waves, nb, lds, s, a); break;
+    case 8: launch_mfma_ns<8>(waves, nb, lds, s, a); break;
+    case 12: launch_mfma_ns<12>(waves, nb, lds, s, a); break;
+    case 16: launch_mfma_ns<16>(waves, nb, lds, s, a); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// abs max of the data (fp16 scaling of the MFMA screen), accumulated over loads
+__global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ X, int64_t nf, float* __restrict__ out) {
+  float m = 0.0f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = fabsf(X[i]);
+    m = (v > m || v != v) ? v : m;  // NaN wins (scale falls back to 1)
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float t = __shfl_xor(m, o);
+    m = (t > m || t != t) ? t : m;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)out, __float_as_uint(m));
+}
+
+hipError_t launch_absmax(const float* X, int64_t nfloats, float* out, hipStream_t s) {
+  if (nfloats <= 0) return hipSuccess;
+  int64_t blocks = (nfloats + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_absmax, dim3((unsigned)blocks), dim3(256), 0, s, X, nfloats, out);
   return hipGetLastError();
 }
 
@@ -695,10 +822,10 @@ __global__ __launch_bounds__(256) void k_rerank2(const float* __restrict__ X, in
 
 static constexpr int FULLSCAN_LDS = 152 * 1024;
 
-__global__ __launch_bounds__(256) void k_fullscan(const float* __restrict__ X, int dp, int d, int k,
-                                                  const double* __restrict__ C64T, const QEntry* __restrict__ queue,
-                                                  const uint32_t* __restrict__ qcount, QLayout ql,
-                                                  int32_t* __restrict__ labels, int use_lds) {
+__global__ __launch_bounds__(1024) void k_fullscan(const float* __restrict__ X, int dp, int d, int k,
+                                                   const double* __restrict__ C64T, const QEntry* __restrict__ queue,
+                                                   const uint32_t* __restrict__ qcount, QLayout ql,
+                                                   int32_t* __restrict__ labels, int use_lds) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sCT = reinterpret_cast<double*>(smem);
   if (use_lds) {
@@ -710,40 +837,48 @@ __global__ __launch_bounds__(256) void k_fullscan(const float* __restrict__ X, i
   const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
   // one wave per segment (grid-stride); each segment's full-scan entries sit
-  // at its back
+  // at its back.  The point's row is held one feature per lane and broadcast
+  // with v_readlane; lanes run over centroids (C64T rows are contiguous in j).
   for (uint32_t sg = gw; sg < ql.nwaves; sg += nw) {
-   const uint32_t cnt = qcount[2 * sg + 1];
-   for (uint32_t e = 0; e < cnt; ++e) {
-    const QEntry* qp = queue + (size_t)sg * ql.seg + (ql.seg - 1u - e);
-    const uint32_t row = __builtin_amdgcn_readfirstlane(qp->row);
-    const float* x = X + (size_t)row * dp;
-    double best = 0.0;
-    int bj = 0x7fffffff;
-    for (int j0 = 0; j0 < k; j0 += 64) {
-      const int j = j0 + lane;
-      if (j < k) {
+    const uint32_t cnt = qcount[2 * sg + 1];
+    for (uint32_t e = 0; e < cnt; ++e) {
+      const QEntry* qp = queue + (size_t)sg * ql.seg + (ql.seg - 1u - e);
+      const uint32_t row = __builtin_amdgcn_readfirstlane(qp->row);
+      const float* x = X + (size_t)row * dp;
+      double best = 0.0;
+      int bj = 0x7fffffff;
+      for (int j0 = 0; j0 < k; j0 += 64) {
+        const int j = min(j0 + lane, k - 1);
         double acc = 0.0;
-        for (int f = 0; f < d; ++f) {
-          const double t = (double)x[f] - CT[(size_t)f * k + j];
-          acc = fma(t, t, acc);
+        for (int f0 = 0; f0 < d; f0 += 64) {
+          const float xl = (f0 + lane < d) ? x[f0 + lane] : 0.0f;
+          const int fe = min(64, d - f0);
+          const double* ct = CT + (size_t)f0 * k + j;
+#pragma unroll 8
+          for (int f = 0; f < 64; ++f) {
+            if (f < fe) {
+              const float xf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xl), f));
+              const double t = (double)xf - ct[(size_t)f * k];
+              acc = fma(t, t, acc);
+            }
+          }
         }
-        if (!(acc != acc) && (bj == 0x7fffffff || acc < best)) {
+        if (j0 + lane < k && !(acc != acc) && (bj == 0x7fffffff || acc < best)) {
           best = acc;
           bj = j;
         }
       }
-    }
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const double ob = __shfl_xor(best, o);
-      const int oj = __shfl_xor(bj, o);
-      if (oj != 0x7fffffff && (bj == 0x7fffffff || ob < best || (ob == best && oj < bj))) {
-        best = ob;
-        bj = oj;
+      for (int o = 32; o >= 1; o >>= 1) {
+        const double ob = __shfl_xor(best, o);
+        const int oj = __shfl_xor(bj, o);
+        if (oj != 0x7fffffff && (bj == 0x7fffffff || ob < best || (ob == best && oj < bj))) {
+          best = ob;
+          bj = oj;
+        }
       }
+      if (lane == 0) labels[row] = (bj == 0x7fffffff) ? 0 : bj;  // all-NaN distances: np.argmin -> 0
     }
-    if (lane == 0) labels[row] = (bj == 0x7fffffff) ? 0 : bj;  // all-NaN distances: np.argmin -> 0
-   }
   }
 }
 
@@ -756,7 +891,7 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   if (e != hipSuccess) return e;
   const size_t bytes = (size_t)g.k * g.d * 8;
   const int use_lds = bytes <= FULLSCAN_LDS ? 1 : 0;
-  hipLaunchKernelGGL(k_fullscan, dim3(n_cu), dim3(256), use_lds ? bytes : 0, s, X, g.dp, g.d, g.k, C64T, queue,
+  hipLaunchKernelGGL(k_fullscan, dim3(n_cu), dim3(1024), use_lds ? bytes : 0, s, X, g.dp, g.d, g.k, C64T, queue,
                      qcount, ql, labels, use_lds);
   return hipGetLastError();
 }

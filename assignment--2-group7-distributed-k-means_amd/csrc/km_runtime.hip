@@ -81,10 +81,13 @@ struct km_ctx {
   double* C64_new = nullptr;
   double* C64T = nullptr;  // transposed [d][k] (full exact scans)
   float* C32 = nullptr;
-  __bf16* Chi = nullptr;
-  __bf16* Clo = nullptr;
-  float* cn2 = nullptr;
-  float* cmax = nullptr;
+  _Float16* Chi = nullptr;  // fp16 hi/lo of -2*c*s [kp][dp]
+  _Float16* Clo = nullptr;
+  float* cn2 = nullptr;      // ||c||^2 (fp32)
+  float* cn2s = nullptr;     // ||c||^2 s^2, pads 1e30
+  float* cmax = nullptr;     // max ||c||
+  float* cabs = nullptr;     // max |c_f|
+  float* xabs = nullptr;     // max |x_f| over the loaded rows
   double* stats_own = nullptr;
   double* stats = nullptr;
   double* work = nullptr;
@@ -141,7 +144,9 @@ void free_centroids(km_ctx* c) {
   dfree(c->Chi);
   dfree(c->Clo);
   dfree(c->cn2);
+  dfree(c->cn2s);
   dfree(c->cmax);
+  dfree(c->cabs);
   dfree(c->stats_own);
   dfree(c->work);
   dfree(c->counts_dev);
@@ -162,6 +167,7 @@ void free_data(km_ctx* c) {
   dfree(c->queue);
   dfree(c->qcount);
   dfree(c->moments);
+  dfree(c->xabs);
   dfree(c->mu);
   dfree(c->sse_base);
   dfree(c->idx_scratch);
@@ -172,7 +178,8 @@ void free_data(km_ctx* c) {
 
 int prep(km_ctx* c) {
   ProfScope ps(c, KM_K_PREP);
-  KM_HIP(km::launch_prep_centroids(c->C64_cur, c->g, c->C32, c->Chi, c->Clo, c->cn2, c->cmax, c->C64T, c->stream));
+  KM_HIP(km::launch_prep_centroids(c->C64_cur, c->g, c->C32, c->cn2, c->cmax, c->cabs, c->C64T, c->stream));
+  KM_HIP(km::launch_prep_split(c->C32, c->g, c->cn2, c->xabs, c->cabs, c->Chi, c->Clo, c->cn2s, c->stream));
   return KM_OK;
 }
 
@@ -198,8 +205,8 @@ int run_assign(km_ctx* c, bool with_stats) {
   }
   {
     ProfScope ps(c, KM_K_ASSIGN);
-    KM_HIP(km::launch_assign_mfma(c->X, g, c->Chi, c->Clo, c->cn2, c->cmax, c->labels, c->queue, c->qcount, c->n_cu,
-                                  &c->ql, c->stream));
+    KM_HIP(km::launch_assign_mfma(c->X, g, c->Chi, c->Clo, c->cn2s, c->cmax, c->xabs, c->cabs, c->labels, c->queue,
+                                  c->qcount, c->n_cu, &c->ql, c->stream));
   }
   {
     ProfScope ps(c, KM_K_RESOLVE);
@@ -320,6 +327,8 @@ int km_load_begin(km_ctx* c, int64_t n, int32_t d) {
   KM_HIP(hipMalloc(&c->queue, sizeof(km::QEntry) * km::queue_capacity(rows, c->n_cu)));
   KM_HIP(hipMalloc(&c->qcount, sizeof(uint32_t) * km::qcount_words(c->n_cu)));
   KM_HIP(hipMalloc(&c->moments, sizeof(double) * (d + 1)));
+  KM_HIP(hipMalloc(&c->xabs, sizeof(float)));
+  KM_HIP(hipMemsetAsync(c->xabs, 0, sizeof(float), c->stream));
   KM_HIP(hipMalloc(&c->mu, sizeof(double) * d));
   KM_HIP(hipMemsetAsync(c->mu, 0, sizeof(double) * d, c->stream));
   KM_HIP(hipMalloc(&c->sse_base, sizeof(double)));
@@ -347,6 +356,7 @@ int km_load_rows(km_ctx* c, int64_t row0, const float* rows, int64_t nrows) {
     memcpy(c->pinned, rows + r * d, sizeof(float) * m * d);
     KM_HIP(hipMemcpy2DAsync(c->X + (row0 + r) * dp, sizeof(float) * dp, c->pinned, sizeof(float) * d,
                             sizeof(float) * d, m, hipMemcpyHostToDevice, c->stream));
+    KM_HIP(km::launch_absmax(c->X + (row0 + r) * dp, m * dp, c->xabs, c->stream));
     KM_HIP(hipStreamSynchronize(c->stream));
   }
   return KM_OK;
@@ -359,6 +369,7 @@ int km_generate_blobs(km_ctx* c, int64_t n, int32_t d, int64_t global_row0, int3
   int rc = km_load_begin(c, n, d);
   if (rc != KM_OK) return rc;
   KM_HIP(km::launch_gen_blobs(c->X, c->g, global_row0, n_centers, box, stddev, seed, c->stream));
+  KM_HIP(km::launch_absmax(c->X, c->g.n * c->g.dp, c->xabs, c->stream));
   KM_HIP(hipStreamSynchronize(c->stream));
   return KM_OK;
 }
@@ -405,16 +416,18 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
     (void)external;
     free_centroids(c);
     c->g.k = k;
-    c->g.kp = (k + 31) / 32 * 32;
+    c->g.kp = (k + 63) / 64 * 64;
     const int kp = c->g.kp, dp = c->g.dp;
     KM_HIP(hipMalloc(&c->C64_cur, sizeof(double) * k * d));
     KM_HIP(hipMalloc(&c->C64_new, sizeof(double) * k * d));
     KM_HIP(hipMalloc(&c->C64T, sizeof(double) * k * d));
     KM_HIP(hipMalloc(&c->C32, sizeof(float) * kp * dp));
-    KM_HIP(hipMalloc(&c->Chi, sizeof(__bf16) * kp * dp));
-    KM_HIP(hipMalloc(&c->Clo, sizeof(__bf16) * kp * dp));
+    KM_HIP(hipMalloc(&c->Chi, sizeof(_Float16) * kp * dp));
+    KM_HIP(hipMalloc(&c->Clo, sizeof(_Float16) * kp * dp));
     KM_HIP(hipMalloc(&c->cn2, sizeof(float) * kp));
+    KM_HIP(hipMalloc(&c->cn2s, sizeof(float) * kp));
     KM_HIP(hipMalloc(&c->cmax, sizeof(float)));
+    KM_HIP(hipMalloc(&c->cabs, sizeof(float)));
     KM_HIP(hipMalloc(&c->stats_own, sizeof(double) * (size_t)k * (d + 1)));
     KM_HIP(hipMalloc(&c->work, sizeof(double) * 3 * k));
     KM_HIP(hipMalloc(&c->counts_dev, sizeof(int64_t) * k));
