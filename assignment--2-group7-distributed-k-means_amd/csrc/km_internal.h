@@ -66,9 +66,22 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
 size_t queue_capacity(int64_t n, int n_cu);
 size_t qcount_words(int n_cu);
 bool mfma_path_ok(const Geometry& g);
+// stats != nullptr: also add the resolved points' rows to the partial sums
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
-                          const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels, int n_cu,
-                          hipStream_t s);
+                          const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
+                          double* stats, int n_cu, hipStream_t s);
+// Fused assign + partial sums (kp*dp <= 16384 class): fp16 hi image in VGPRs,
+// lo image + float64 sum table in LDS; decided points summed here, queued
+// points by launch_resolve(stats), sizes by launch_count.
+bool fused_path_ok(const Geometry& g);
+hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, const _Float16* Chi,
+                        const _Float16* Clo, uint4* ChiF, uint4* CloF, const float* cn2s, const float* bnd,
+                        const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,
+                        double* stats, int with_stats, int n_cu, QLayout* ql, hipStream_t s);
+hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float* cabs, int dp, float* bnd,
+                               hipStream_t s);
+hipError_t launch_row_norm(const float* X, const Geometry& g, float* xnorm, hipStream_t s);
+hipError_t launch_count(const int32_t* labels, const Geometry& g, double* stats, int n_cu, hipStream_t s);
 hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels, double* stats, int n_cu,
                         hipStream_t s);
 hipError_t launch_update(const double* stats, const double* C64_old, const double* mu, const Geometry& g,

@@ -739,6 +739,474 @@ hipError_t launch_absmax(const float* X, int64_t nfloats, float* out, hipStream_
 }
 
 // ---------------------------------------------------------------------------
+// Fused assign + partial statistics (c3 class: kp*dp <= 16384).
+//
+// One workgroup of 8 waves per CU (2 per SIMD).  The fp16 hi image of
+// -2*c*s lives in VGPRs (A fragments, NB*NS*4 registers per lane), the lo
+// image in LDS (NB*NS KiB, fragment-linear), and the rest of LDS holds this
+// workgroup's float64 partial sums, transposed [f][j] so that the 32 lanes
+// of one ds_add_f64 (32 points, one feature) hit banks j mod 32.  Each wave
+// walks 32-point tiles: fp16x3 MFMA scores, four chains of top-2 keys
+// (score | j>>2), merged to the top-3 values and the best two indices, the
+// rigorous screening bound, label + ambiguous-point queue, and for every
+// decided point its exact fp32 row added to the table.  Ambiguous points are
+// added by the resolver kernels, counts by k_count over the final labels.
+// The table is flushed with one float64 atomic per non-zero entry.
+// ---------------------------------------------------------------------------
+struct FusedArgs {
+  const float* X;
+  const float* xnorm;  // per-row upper bound of ||x|| (unscaled)
+  int64_t n;
+  int k, d;
+  uint32_t seg;
+  const uint4* ChiF;   // fragment-linear hi image [NB][NS][64] x 16 B
+  const uint4* CloF;   // fragment-linear lo image
+  const float* cn2s;   // ||c||^2 s^2 [kp], pads 1e30
+  const float* bnd;    // B0 = bnd[0] * ||x|| + bnd[1]
+  const float* xabs;
+  const float* cabs;
+  int32_t* labels;
+  QEntry* queue;
+  uint32_t* qcount;
+  double* stats;       // [k][d+1] (sums; counts by k_count)
+};
+
+constexpr int ceil_log2_c(int v) { return v <= 1 ? 0 : 1 + ceil_log2_c((v + 1) / 2); }
+
+__device__ __forceinline__ void perm_halves(uint32_t v, uint32_t& lo, uint32_t& hi) {
+  // lo = value of lane (l & 31), hi = value of lane (l | 32), in every lane
+  const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  lo = p[0];
+  hi = p[1];
+}
+
+// ABL (diagnostic builds, KM_ABLATE=1..4, c3 shape only; results wrong):
+// 1 = no key updates, 2 = no MFMAs, 3 = no LDS sums, 4 = no merge / queue,
+// 5 = MFMAs + conversion + loads only
+template <int NS, int NB, bool STATS, int ABL = 0>
+__global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
+  constexpr int DP = 16 * NS;
+  constexpr int KP = 32 * NB;
+  constexpr int WAVES = 4;
+  constexpr int B = ceil_log2_c(KP);
+  static_assert(B >= 3 && B - 2 <= 12, "index bits");
+  static_assert(NB >= 2, "pipelined blocks");
+  constexpr uint32_t maskq = (1u << (B - 2)) - 1u;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* sCn = reinterpret_cast<float*>(smem);                  // ||c||^2 s^2 [KP]
+  double* tab = reinterpret_cast<double*>(smem + KP * 4);        // [DP][KP]
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  for (int i = threadIdx.x; i < KP; i += WAVES * 64) sCn[i] = A.cn2s[i];
+  if constexpr (STATS)
+    for (int i = threadIdx.x; i < DP * KP; i += WAVES * 64) tab[i] = 0.0;
+  f16x8 Ahi[NB][NS], Alo[NB][NS];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      Ahi[b][t] = __builtin_bit_cast(f16x8, A.ChiF[(b * NS + t) * 64 + lane]);
+      Alo[b][t] = __builtin_bit_cast(f16x8, A.CloF[(b * NS + t) * 64 + lane]);
+    }
+  __syncthreads();
+
+  const float s = mfma_scale(*A.xabs, *A.cabs);
+  const float alpha = A.bnd[0], beta = A.bnd[1];
+  const float rho = __builtin_ldexpf(1.0f, B - 2 - 23) * 1.01f;
+  const int64_t n = A.n;
+  const int64_t ntiles = (n + 31) / 32;
+  const uint32_t gw = blockIdx.x * WAVES + wave;
+  QEntry* wq = A.queue + (size_t)gw * A.seg;
+  uint32_t qn = 0, qf = 0;
+  const int64_t tstride = (int64_t)gridDim.x * WAVES;
+  const float4* cnl = reinterpret_cast<const float4*>(sCn + 4 * h);  // + 8 blk + 2 g4
+
+  auto load_tile = [&](int64_t tile, float4 (&xq)[NS][2], float& xnq) {
+    const int64_t row = tile * 32 + r;
+    const int64_t rr = row < n ? row : (n - 1);
+    const float* xr = A.X + rr * DP + 8 * h;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      xq[t][0] = *reinterpret_cast<const float4*>(xr + 16 * t);
+      xq[t][1] = *reinterpret_cast<const float4*>(xr + 16 * t + 4);
+    }
+    xnq = A.xnorm[rr];
+  };
+
+  auto process_tile = [&](int64_t tile, const float4 (&xc)[NS][2], float xn) {
+    const int64_t row = tile * 32 + r;
+    const bool valid = row < n;
+    // B operand: lane (r, h) holds features [16t + 8h, +8) of point r,
+    // split xs = hi + lo (fp16, RN)
+    f16x8 bh[NS], bl[NS];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      const float xv[8] = {xc[t][0].x, xc[t][0].y, xc[t][0].z, xc[t][0].w,
+                           xc[t][1].x, xc[t][1].y, xc[t][1].z, xc[t][1].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xs = xv[e] * s;
+        const _Float16 hi = (_Float16)xs;
+        bh[t][e] = hi;
+        bl[t][e] = (_Float16)(xs - (float)hi);
+      }
+    }
+    float a1[4], a2[4], a3[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a1[c] = a2[c] = a3[c] = FLT_MAX;
+    // the images stay in AGPRs (MFMA A operands read them there); scores
+    // land in VGPRs (built with -amdgpu-mfma-vgpr-form)
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int t = 0; t < NS; ++t) asm volatile("" : "+a"(Ahi[b][t]), "+a"(Alo[b][t]));
+    auto cn_init = [&](int blk) {
+      f32x16 acc;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 cv = cnl[8 * blk + 2 * g4];
+        acc[4 * g4 + 0] = cv.x;
+        acc[4 * g4 + 1] = cv.y;
+        acc[4 * g4 + 2] = cv.z;
+        acc[4 * g4 + 3] = cv.w;
+      }
+      return acc;
+    };
+    auto mfma_block = [&](f32x16 acc, int blk) {
+      if constexpr (ABL == 2) {
+#pragma unroll
+        for (int t = 0; t < NS; ++t) acc[t] += (float)Ahi[blk][t][0] + (float)Alo[blk][t][1] + (float)bl[t][2] + (float)bh[t][3];
+        return acc;
+      }
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bl[t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Alo[blk][t], bh[t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bh[t], acc, 0, 0, 0);
+      }
+      return acc;
+    };
+    // register reg holds centroid j = 32 blk + 4h + (reg & 3) + 8 (reg >> 2);
+    // chain reg & 3 keeps the top three keys (score | j >> 2)
+    auto keys_block = [&](const f32x16& acc, int blk) {
+      if constexpr (ABL == 1 || ABL == 5) {
+        a1[blk & 3] = fminf(a1[blk & 3], acc[0] + acc[15]);
+        asm volatile("" ::"v"(acc));
+        return;
+      }
+      const uint32_t jq = (uint32_t)(8 * blk + h);
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const float key = __uint_as_float((__float_as_uint(acc[reg]) & ~maskq) | (jq | (uint32_t)(2 * (reg >> 2))));
+        top3_insert(a1[reg & 3], a2[reg & 3], a3[reg & 3], key);
+      }
+    };
+    // software pipeline: block blk's MFMAs overlap block blk-1's key
+    // updates (started two MFMAs in, once blk-1's scores have landed); the
+    // accumulator init of block blk+1 is read from LDS meanwhile
+    f32x16 accs[2];
+    f32x16 cinit = cn_init(1);
+    accs[0] = mfma_block(cn_init(0), 0);
+#pragma unroll
+    for (int blk = 1; blk < NB; ++blk) {
+      const f32x16 cin = cinit;
+      if (blk + 1 < NB) cinit = cn_init(blk + 1);
+      accs[blk & 1] = mfma_block(cin, blk);
+      keys_block(accs[(blk - 1) & 1], blk - 1);
+      // MFMA, next block's init reads, MFMA, then (VALU x m, MFMA) pairs
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+#pragma unroll
+      for (int i = 0; i < 3 * NS - 2; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x2, 64 / (3 * NS - 2) + 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    keys_block(accs[(NB - 1) & 1], NB - 1);
+
+    if constexpr (ABL == 5) {
+      const int lab = (int)(__float_as_uint(a1[0] + a1[1] + a1[2] + a1[3] + xn) & 255u) % A.k;
+      if (h == 0 && valid) A.labels[row] = lab;
+      return;
+    }
+    if constexpr (ABL == 4) {
+      const int lab = (int)(__float_as_uint(a1[0] + a1[1] + a1[2] + a1[3] + a2[0] + a2[1] + a2[2] + a2[3] + xn) & 255u) % A.k;
+      if (h == 0 && valid) A.labels[row] = lab;
+      if constexpr (STATS) {
+        double* tp = tab + (size_t)(8 * h) * KP + lab;
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+          const float4 v0 = xc[t][0], v1 = xc[t][1];
+          const float xe[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) atomicAdd(tp + (size_t)(16 * t + e) * KP, (double)xe[e]);
+        }
+      }
+      return;
+    }
+    // lane-local top-3 values and best two full indices over the kept keys
+    // (a chain's third never enters the top two)
+    float k1 = FLT_MAX, k2 = FLT_MAX, k3 = FLT_MAX;
+    uint32_t p1 = 0, p2 = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      top3p_insert(k1, k2, k3, p1, p2, a1[c], ((__float_as_uint(a1[c]) & maskq) << 2) | (uint32_t)c);
+      top3p_insert(k1, k2, k3, p1, p2, a2[c], ((__float_as_uint(a2[c]) & maskq) << 2) | (uint32_t)c);
+      top3p_insert(k1, k2, k3, p1, p2, a3[c], 0u);
+    }
+    {  // merge the two lane halves (disjoint centroid rows of the same point)
+      uint32_t K1, Q1, K2, Q2, K3, Q3, P1, R1, P2, R2;
+      perm_halves(__float_as_uint(k1), K1, Q1);
+      perm_halves(__float_as_uint(k2), K2, Q2);
+      perm_halves(__float_as_uint(k3), K3, Q3);
+      perm_halves(p1, P1, R1);
+      perm_halves(p2, P2, R2);
+      const float fK1 = __uint_as_float(K1), fQ1 = __uint_as_float(Q1);
+      const float fK2 = __uint_as_float(K2), fQ2 = __uint_as_float(Q2);
+      const float fK3 = __uint_as_float(K3), fQ3 = __uint_as_float(Q3);
+      const bool takeK = fK1 <= fQ1;
+      k1 = takeK ? fK1 : fQ1;
+      p1 = takeK ? P1 : R1;
+      const float sa = takeK ? fK2 : fK1;   // candidates for the second
+      const float sb = takeK ? fQ1 : fQ2;
+      const uint32_t ia = takeK ? P2 : P1;
+      const uint32_t ib = takeK ? R1 : R2;
+      const bool ta = sa <= sb;
+      k2 = ta ? sa : sb;
+      p2 = ta ? ia : ib;
+      k3 = fminf(fminf(fK3, fQ3), fminf(fmaxf(fK1, fQ2), fmaxf(fK2, fQ1)));
+    }
+    // every candidate other than p1, p2 is >= k3 (a chain drops only keys
+    // above its kept third)
+    const float B0 = fmaf(alpha, xn, beta);
+    const float thr2 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k2));
+    const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k3));
+    uint32_t kind = 0;
+    if (!(k3 - k1 > thr3))
+      kind = 2;
+    else if (!(k2 - k1 > thr2))
+      kind = 1;
+    const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
+    if (h == 0 && valid) A.labels[row] = lab;
+    const bool enq = (h == 0) && valid && (kind != 0);
+    const uint64_t m = __ballot(enq);
+    if (m) {
+      const uint64_t m1 = __ballot(enq && kind == 1);
+      const uint64_t m2 = m & ~m1;
+      const uint64_t below = (1ull << lane) - 1ull;
+      if (enq) {
+        QEntry q;
+        q.row = (uint32_t)row;
+        q.i1 = p1;
+        q.i2 = p2;
+        q.kind = kind;
+        const uint32_t pos = (kind == 1) ? qn + (uint32_t)__popcll(m1 & below)
+                                         : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
+        wq[pos] = q;
+      }
+      qn += (uint32_t)__popcll(m1);
+      qf += (uint32_t)__popcll(m2);
+    }
+    if constexpr (STATS && ABL != 3) {
+      if (valid && kind == 0) {
+        double* tp = tab + (size_t)(8 * h) * KP + lab;
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+          const float4 v0 = xc[t][0], v1 = xc[t][1];
+          const float xe[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) atomicAdd(tp + (size_t)(16 * t + e) * KP, (double)xe[e]);
+        }
+      }
+    }
+    };
+
+  // tiles of this wave, two register buffers: the next tile's rows are in
+  // flight while this one is processed
+  float4 xb0[NS][2], xb1[NS][2];
+  float xn0 = 0.0f, xn1 = 0.0f;
+  if ((int64_t)gw < ntiles) load_tile(gw, xb0, xn0);
+  for (int64_t tile = gw; tile < ntiles; tile += 2 * tstride) {
+    const int64_t t1 = tile + tstride;
+    if (t1 < ntiles) load_tile(t1, xb1, xn1);
+    process_tile(tile, xb0, xn0);
+    if (t1 >= ntiles) break;
+    if (t1 + tstride < ntiles) load_tile(t1 + tstride, xb0, xn0);
+    process_tile(t1, xb1, xn1);
+  }
+  if (lane == 0) {
+    A.qcount[2 * gw] = qn;
+    A.qcount[2 * gw + 1] = qf;
+  }
+  if constexpr (STATS) {
+    __syncthreads();
+    const int d1 = A.d + 1;
+    // row-major walk of the global [k][d+1] buffer: a wave's atomics cover
+    // contiguous bytes (scattered float64 atomics run ~17x slower)
+    for (int i = threadIdx.x; i < DP * KP; i += WAVES * 64) {
+      const int j = i / DP;
+      const int f = i - j * DP;
+      const double v = tab[(size_t)f * KP + j];
+      if (v != 0.0 && f < A.d && j < A.k) atomicAdd(A.stats + (size_t)j * d1 + f, v);
+    }
+  }
+}
+
+// fragment-linear copies of the hi / lo images: piece (b, t), lane l holds
+// 8 halves of row 32 b + (l & 31), features 16 t + 8 (l >> 5) .. + 8
+__global__ __launch_bounds__(256) void k_frag_images(const _Float16* __restrict__ Chi, const _Float16* __restrict__ Clo,
+                                                     int kp, int dp, uint4* __restrict__ ChiF,
+                                                     uint4* __restrict__ CloF) {
+  const int ns = dp / 16;
+  const int total = (kp / 32) * ns * 64;
+  const int id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= total) return;
+  const int l = id & 63;
+  const int bt = id >> 6;
+  const int b = bt / ns, t = bt - b * ns;
+  const size_t src = (size_t)(b * 32 + (l & 31)) * dp + 16 * t + 8 * (l >> 5);
+  ChiF[id] = *reinterpret_cast<const uint4*>(Chi + src);
+  CloF[id] = *reinterpret_cast<const uint4*>(Clo + src);
+}
+
+// screening-bound constants: B0 = alpha * ||x|| + beta (see k_assign_mfma)
+__global__ void k_bound_consts(const float* __restrict__ cmax, const float* __restrict__ xabs,
+                               const float* __restrict__ cabs, int dp, float* __restrict__ bnd) {
+  const float s = mfma_scale(*xabs, *cabs);
+  const float cm = *cmax * s;
+  const float sq = sqrtf((float)dp);
+  bnd[0] = 1.5f * s * ((6.5f * 2.384185791015625e-07f + 0.5f * U24 + (float)(6 * dp + 8) * U24) * cm + U24 * sq);
+  bnd[1] = 1.5f * ((float)(3 * dp + 5) * U24 * cm * cm + 2.0f * U24 * sq * cm);
+}
+
+// upper bound of ||x|| per row (float64 sum, rounded up)
+__global__ __launch_bounds__(256) void k_row_norm(const float* __restrict__ X, int64_t n, int dp,
+                                                  float* __restrict__ xnorm) {
+  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < n;
+       row += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int f = 0; f < dp; ++f) {
+      const double v = X[row * dp + f];
+      s = fma(v, v, s);
+    }
+    xnorm[row] = (float)(sqrt(s) * (1.0 + 1e-6)) * 1.0000001f;
+  }
+}
+
+// cluster sizes from the final labels into the count column of stats
+__global__ __launch_bounds__(1024) void k_count(const int32_t* __restrict__ labels, int64_t n, int k,
+                                                double* __restrict__ stats, int d) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
+  for (int i = threadIdx.x; i < k; i += blockDim.x) hist[i] = 0u;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int l = labels[i];
+    if ((unsigned)l < (unsigned)k) atomicAdd(hist + l, 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < k; i += blockDim.x)
+    if (hist[i]) atomicAdd(stats + (size_t)i * (d + 1) + d, (double)hist[i]);
+}
+
+bool fused_path_ok(const Geometry& g) {
+  const int ns = g.dp / 16, nb = g.kp / 32;
+  if (g.dp % 16 || g.kp % 64) return false;
+  switch (ns * 100 + nb) {
+    case 402: case 404: case 406: case 408:
+    case 202: case 204: case 206: case 208: case 212: case 216:
+    case 302: case 304: case 306: case 308:
+    case 802: case 804:
+      return true;
+    default:
+      return false;
+  }
+}
+
+hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, const _Float16* Chi,
+                        const _Float16* Clo, uint4* ChiF, uint4* CloF, const float* cn2s, const float* bnd,
+                        const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,
+                        double* stats, int with_stats, int n_cu, QLayout* ql, hipStream_t s) {
+  ql->seg = 0;
+  ql->nwaves = 0;
+  if (g.n == 0) return hipSuccess;
+  const int ns = g.dp / 16, nb = g.kp / 32;
+  {
+    const int total = nb * ns * 64;
+    hipLaunchKernelGGL(k_frag_images, dim3((total + 255) / 256), dim3(256), 0, s, Chi, Clo, g.kp, g.dp, ChiF, CloF);
+  }
+  constexpr int WAVES = 4;
+  const int64_t ntiles = (g.n + 31) / 32;
+  int64_t blocks = n_cu;
+  if (blocks > (ntiles + WAVES - 1) / WAVES) blocks = (ntiles + WAVES - 1) / WAVES;
+  const int nbk = (int)blocks;
+  const int64_t nw = (int64_t)nbk * WAVES;
+  const uint32_t seg = (uint32_t)(((ntiles + nw - 1) / nw) * 32);
+  ql->seg = seg;
+  ql->nwaves = (uint32_t)nw;
+  FusedArgs a{X, xnorm, g.n, g.k, g.d, seg, ChiF, CloF, cn2s, bnd, xabs, cabs, labels, queue, qcount, stats};
+  const size_t lds = (size_t)g.kp * 4 + (with_stats ? (size_t)g.dp * g.kp * 8 : 0);
+#define KM_FUSED_CASE(NS_, NB_)                                                                        \
+  case NS_ * 100 + NB_:                                                                                \
+    if (with_stats)                                                                                    \
+      hipLaunchKernelGGL((k_fused<NS_, NB_, true>), dim3(nbk), dim3(256), lds, s, a);                  \
+    else                                                                                               \
+      hipLaunchKernelGGL((k_fused<NS_, NB_, false>), dim3(nbk), dim3(256), lds, s, a);                 \
+    break;
+  {
+    static const char* abl = getenv("KM_ABLATE");
+    if (abl && ns == 4 && nb == 8 && with_stats && abl[0] >= '1' && abl[0] <= '5') {
+      switch (abl[0]) {
+        case '1': hipLaunchKernelGGL((k_fused<4, 8, true, 1>), dim3(nbk), dim3(256), lds, s, a); break;
+        case '2': hipLaunchKernelGGL((k_fused<4, 8, true, 2>), dim3(nbk), dim3(256), lds, s, a); break;
+        case '3': hipLaunchKernelGGL((k_fused<4, 8, true, 3>), dim3(nbk), dim3(256), lds, s, a); break;
+        case '5': hipLaunchKernelGGL((k_fused<4, 8, true, 5>), dim3(nbk), dim3(256), lds, s, a); break;
+        default: hipLaunchKernelGGL((k_fused<4, 8, true, 4>), dim3(nbk), dim3(256), lds, s, a); break;
+      }
+      return hipGetLastError();
+    }
+  }
+  switch (ns * 100 + nb) {
+    KM_FUSED_CASE(4, 2) KM_FUSED_CASE(4, 4) KM_FUSED_CASE(4, 6) KM_FUSED_CASE(4, 8)
+    KM_FUSED_CASE(2, 2) KM_FUSED_CASE(2, 4) KM_FUSED_CASE(2, 6) KM_FUSED_CASE(2, 8) KM_FUSED_CASE(2, 12)
+    KM_FUSED_CASE(2, 16)
+    KM_FUSED_CASE(3, 2) KM_FUSED_CASE(3, 4) KM_FUSED_CASE(3, 6) KM_FUSED_CASE(3, 8)
+    KM_FUSED_CASE(8, 2) KM_FUSED_CASE(8, 4)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef KM_FUSED_CASE
+  return hipGetLastError();
+}
+
+hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float* cabs, int dp, float* bnd,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(k_bound_consts, dim3(1), dim3(1), 0, s, cmax, xabs, cabs, dp, bnd);
+  return hipGetLastError();
+}
+
+hipError_t launch_row_norm(const float* X, const Geometry& g, float* xnorm, hipStream_t s) {
+  if (g.n == 0) return hipSuccess;
+  int64_t blocks = (g.n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_row_norm, dim3((unsigned)blocks), dim3(256), 0, s, X, g.n, g.dp, xnorm);
+  return hipGetLastError();
+}
+
+hipError_t launch_count(const int32_t* labels, const Geometry& g, double* stats, int n_cu, hipStream_t s) {
+  if (g.n == 0) return hipSuccess;
+  int64_t blocks = (g.n + 1023) / 1024;
+  if (blocks > n_cu) blocks = n_cu;
+  hipLaunchKernelGGL(k_count, dim3((unsigned)blocks), dim3(1024), (size_t)g.k * 4, s, labels, g.n, g.k, stats, g.d);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Exact float64 resolution of the queued ambiguous points (np.argmin with
 // first-minimum tie-break, kmeans_spark.py:153-156).
 //   k_rerank2:   {i1, i2} re-ranked, 16 lanes per entry (4 entries per wave,
@@ -748,10 +1216,21 @@ hipError_t launch_absmax(const float* X, int64_t nfloats, float* out, hipStream_
 //                they fit (read from L2 otherwise).
 // Walks the per-wave queue segments written by k_assign_mfma.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_rerank2(const float* __restrict__ X, int dp, int d, int k,
-                                                 const double* __restrict__ C64, const QEntry* __restrict__ queue,
-                                                 const uint32_t* __restrict__ qcount, QLayout ql,
-                                                 int32_t* __restrict__ labels) {
+// With stats != nullptr the resolved points' rows are added to the partial
+// sums (the fused kernel leaves every queued point to the resolvers): into an
+// LDS table [f][j] flushed at the end when it fits (tab_kp > 0), else with
+// global float64 atomics.
+__global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, int dp, int d, int k,
+                                                  const double* __restrict__ C64, const QEntry* __restrict__ queue,
+                                                  const uint32_t* __restrict__ qcount, QLayout ql,
+                                                  int32_t* __restrict__ labels, double* __restrict__ stats,
+                                                  int tab_kp) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* tab = reinterpret_cast<double*>(smem);
+  if (stats && tab_kp) {
+    for (int i = threadIdx.x; i < d * tab_kp; i += blockDim.x) tab[i] = 0.0;
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63;
   const int sub = lane >> 4;   // entry slot in the wave
   const int m = lane & 15;     // features 4m..4m+3 (+64t)
@@ -793,12 +1272,30 @@ __global__ __launch_bounds__(256) void k_rerank2(const float* __restrict__ X, in
         s1 += __shfl_xor(s1, o);
         s2 += __shfl_xor(s2, o);
       }
-      if (ok && m == 0) {
+      int lab = -1;
+      if (ok) {
         const bool first_a = q.i1 < q.i2;
         const int a = (int)(first_a ? q.i1 : q.i2), bb = (int)(first_a ? q.i2 : q.i1);
         const double sa = first_a ? s1 : s2, sb = first_a ? s2 : s1;
-        labels[q.row] = (sb < sa) ? bb : a;  // ties and NaN keep the lower index
-      } else if (have && !ok && m == 0) {
+        lab = (sb < sa) ? bb : a;  // ties and NaN keep the lower index
+        if (m == 0) labels[q.row] = lab;
+      }
+      if (ok && stats) {
+        const float* x = X + (size_t)q.row * dp;
+        for (int f0 = 4 * m; f0 < d; f0 += 64) {
+          const float4 xv = *reinterpret_cast<const float4*>(x + f0);
+          const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (f0 + c < d) {
+              if (tab_kp)
+                atomicAdd(tab + (size_t)(f0 + c) * tab_kp + lab, (double)xs[c]);
+              else
+                atomicAdd(stats + (size_t)lab * (d + 1) + f0 + c, (double)xs[c]);
+            }
+        }
+      }
+      if (have && !ok && m == 0) {
         // corrupt candidate (cannot happen for finite data): exact scan
         const float* x = X + (size_t)q.row * dp;
         double best = 0.0;
@@ -815,7 +1312,19 @@ __global__ __launch_bounds__(256) void k_rerank2(const float* __restrict__ X, in
           }
         }
         labels[q.row] = bl;
+        if (stats) {
+          for (int f = 0; f < d; ++f) atomicAdd(stats + (size_t)bl * (d + 1) + f, (double)x[f]);
+        }
       }
+    }
+  }
+  if (stats && tab_kp) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < d * tab_kp; i += blockDim.x) {
+      const int j = i / d;
+      const int f = i - j * d;
+      const double v = tab[(size_t)f * tab_kp + j];
+      if (v != 0.0 && j < k) atomicAdd(stats + (size_t)j * (d + 1) + f, v);
     }
   }
 }
@@ -825,7 +1334,8 @@ static constexpr int FULLSCAN_LDS = 152 * 1024;
 __global__ __launch_bounds__(1024) void k_fullscan(const float* __restrict__ X, int dp, int d, int k,
                                                    const double* __restrict__ C64T, const QEntry* __restrict__ queue,
                                                    const uint32_t* __restrict__ qcount, QLayout ql,
-                                                   int32_t* __restrict__ labels, int use_lds) {
+                                                   int32_t* __restrict__ labels, int use_lds,
+                                                   double* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sCT = reinterpret_cast<double*>(smem);
   if (use_lds) {
@@ -839,9 +1349,14 @@ __global__ __launch_bounds__(1024) void k_fullscan(const float* __restrict__ X, 
   // one wave per segment (grid-stride); each segment's full-scan entries sit
   // at its back.  The point's row is held one feature per lane and broadcast
   // with v_readlane; lanes run over centroids (C64T rows are contiguous in j).
-  for (uint32_t sg = gw; sg < ql.nwaves; sg += nw) {
+  // entries of all segments are spread over all waves (entry e of segment
+  // sg goes to wave (e + 7919 sg) mod nw): segments hold a few entries each,
+  // and a wave per segment would leave most waves idle with the dependent
+  // queue -> row -> data loads exposed)
+  for (uint32_t sg = 0; sg < ql.nwaves; ++sg) {
     const uint32_t cnt = qcount[2 * sg + 1];
-    for (uint32_t e = 0; e < cnt; ++e) {
+    const uint32_t first = (gw + nw - (uint32_t)(((uint64_t)sg * 7919u) % nw)) % nw;
+    for (uint32_t e = first; e < cnt; e += nw) {
       const QEntry* qp = queue + (size_t)sg * ql.seg + (ql.seg - 1u - e);
       const uint32_t row = __builtin_amdgcn_readfirstlane(qp->row);
       const float* x = X + (size_t)row * dp;
@@ -877,22 +1392,28 @@ __global__ __launch_bounds__(1024) void k_fullscan(const float* __restrict__ X, 
           bj = oj;
         }
       }
-      if (lane == 0) labels[row] = (bj == 0x7fffffff) ? 0 : bj;  // all-NaN distances: np.argmin -> 0
+      const int lab = (bj == 0x7fffffff) ? 0 : bj;  // all-NaN distances: np.argmin -> 0
+      if (lane == 0) labels[row] = lab;
+      if (stats)
+        for (int f = lane; f < d; f += 64) atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)x[f]);
     }
   }
 }
 
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
-                          const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels, int n_cu,
-                          hipStream_t s) {
+                          const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
+                          double* stats, int n_cu, hipStream_t s) {
   if (g.n == 0 || ql.nwaves == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rerank2, dim3(n_cu * 8), dim3(256), 0, s, X, g.dp, g.d, g.k, C64, queue, qcount, ql, labels);
+  const size_t tab_bytes = (size_t)g.d * g.kp * 8;
+  const int tab_kp = (stats && tab_bytes <= FULLSCAN_LDS) ? g.kp : 0;
+  hipLaunchKernelGGL(k_rerank2, dim3(n_cu), dim3(1024), tab_kp ? tab_bytes : 0, s, X, g.dp, g.d, g.k, C64, queue,
+                     qcount, ql, labels, stats, tab_kp);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t bytes = (size_t)g.k * g.d * 8;
   const int use_lds = bytes <= FULLSCAN_LDS ? 1 : 0;
   hipLaunchKernelGGL(k_fullscan, dim3(n_cu), dim3(1024), use_lds ? bytes : 0, s, X, g.dp, g.d, g.k, C64T, queue,
-                     qcount, ql, labels, use_lds);
+                     qcount, ql, labels, use_lds, stats);
   return hipGetLastError();
 }
 

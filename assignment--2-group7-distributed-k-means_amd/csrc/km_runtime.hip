@@ -3,6 +3,7 @@
 // One km_ctx per GPU (one process per GPU, torch.distributed ranks).  All
 // per-iteration work is enqueued on ctx->stream; only calls that hand host
 // data back synchronise it.  See DESIGN.md for the data layout in HBM.
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -47,6 +48,13 @@ void hfree(T*& p) {
 
 constexpr int kAllowedDp[] = {16, 32, 48, 64, 96, 128, 192, 256};
 
+// KM_FUSED=0 selects the two-pass MFMA path (screen, then a statistics pass)
+// for the shapes the fused kernel covers (A/B measurements)
+bool fused_disabled() {
+  const char* e = getenv("KM_FUSED");
+  return e && e[0] == '0';
+}
+
 int choose_dp(int d) {
   for (int v : kAllowedDp)
     if (d <= v) return v;
@@ -63,6 +71,7 @@ struct km_ctx {
   bool loaded = false;
   bool have_c = false;
   int path = 0;  // 1 small, 2 mfma
+  bool fused = false;  // path 2 with the fused assign + sums kernel
   // data
   float* X = nullptr;
   int32_t* labels = nullptr;
@@ -88,6 +97,10 @@ struct km_ctx {
   float* cmax = nullptr;     // max ||c||
   float* cabs = nullptr;     // max |c_f|
   float* xabs = nullptr;     // max |x_f| over the loaded rows
+  float* xnorm = nullptr;    // per-row upper bound of ||x|| (screening bound)
+  uint4* ChiF = nullptr;     // fragment-linear hi / lo images (fused kernel)
+  uint4* CloF = nullptr;
+  float* bnd = nullptr;      // screening-bound constants
   double* stats_own = nullptr;
   double* stats = nullptr;
   double* work = nullptr;
@@ -145,6 +158,9 @@ void free_centroids(km_ctx* c) {
   dfree(c->Clo);
   dfree(c->cn2);
   dfree(c->cn2s);
+  dfree(c->ChiF);
+  dfree(c->CloF);
+  dfree(c->bnd);
   dfree(c->cmax);
   dfree(c->cabs);
   dfree(c->stats_own);
@@ -168,6 +184,7 @@ void free_data(km_ctx* c) {
   dfree(c->qcount);
   dfree(c->moments);
   dfree(c->xabs);
+  dfree(c->xnorm);
   dfree(c->mu);
   dfree(c->sse_base);
   dfree(c->idx_scratch);
@@ -180,6 +197,7 @@ int prep(km_ctx* c) {
   ProfScope ps(c, KM_K_PREP);
   KM_HIP(km::launch_prep_centroids(c->C64_cur, c->g, c->C32, c->cn2, c->cmax, c->cabs, c->C64T, c->stream));
   KM_HIP(km::launch_prep_split(c->C32, c->g, c->cn2, c->xabs, c->cabs, c->Chi, c->Clo, c->cn2s, c->stream));
+  KM_HIP(km::launch_bound_consts(c->cmax, c->xabs, c->cabs, c->g.dp, c->bnd, c->stream));
   return KM_OK;
 }
 
@@ -203,6 +221,24 @@ int run_assign(km_ctx* c, bool with_stats) {
                                    c->n_cu, c->stream));
     return KM_OK;
   }
+  if (c->fused) {
+    {
+      ProfScope ps(c, KM_K_ASSIGN);
+      KM_HIP(km::launch_fused(c->X, c->xnorm, g, c->Chi, c->Clo, c->ChiF, c->CloF, c->cn2s, c->bnd, c->xabs, c->cabs,
+                              c->labels, c->queue, c->qcount, c->stats, with_stats ? 1 : 0, c->n_cu, &c->ql,
+                              c->stream));
+    }
+    {
+      ProfScope ps(c, KM_K_RESOLVE);
+      KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels,
+                                with_stats ? c->stats : nullptr, c->n_cu, c->stream));
+    }
+    if (with_stats) {
+      ProfScope ps(c, KM_K_STATS);
+      KM_HIP(km::launch_count(c->labels, g, c->stats, c->n_cu, c->stream));
+    }
+    return KM_OK;
+  }
   {
     ProfScope ps(c, KM_K_ASSIGN);
     KM_HIP(km::launch_assign_mfma(c->X, g, c->Chi, c->Clo, c->cn2s, c->cmax, c->xabs, c->cabs, c->labels, c->queue,
@@ -210,7 +246,8 @@ int run_assign(km_ctx* c, bool with_stats) {
   }
   {
     ProfScope ps(c, KM_K_RESOLVE);
-    KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels, c->n_cu, c->stream));
+    KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels, nullptr, c->n_cu,
+                              c->stream));
   }
   if (with_stats) {
     ProfScope ps(c, KM_K_STATS);
@@ -304,7 +341,7 @@ int km_info_get(km_ctx* c, km_info* out) {
   out->path = c->path;
   out->n_cu = c->n_cu;
   out->device = c->device;
-  out->fused_stats = (c->path == 1);
+  out->fused_stats = (c->path == 1) || c->fused;
   return KM_OK;
 }
 
@@ -328,6 +365,7 @@ int km_load_begin(km_ctx* c, int64_t n, int32_t d) {
   KM_HIP(hipMalloc(&c->qcount, sizeof(uint32_t) * km::qcount_words(c->n_cu)));
   KM_HIP(hipMalloc(&c->moments, sizeof(double) * (d + 1)));
   KM_HIP(hipMalloc(&c->xabs, sizeof(float)));
+  KM_HIP(hipMalloc(&c->xnorm, sizeof(float) * rows));
   KM_HIP(hipMemsetAsync(c->xabs, 0, sizeof(float), c->stream));
   KM_HIP(hipMalloc(&c->mu, sizeof(double) * d));
   KM_HIP(hipMemsetAsync(c->mu, 0, sizeof(double) * d, c->stream));
@@ -357,6 +395,9 @@ int km_load_rows(km_ctx* c, int64_t row0, const float* rows, int64_t nrows) {
     KM_HIP(hipMemcpy2DAsync(c->X + (row0 + r) * dp, sizeof(float) * dp, c->pinned, sizeof(float) * d,
                             sizeof(float) * d, m, hipMemcpyHostToDevice, c->stream));
     KM_HIP(km::launch_absmax(c->X + (row0 + r) * dp, m * dp, c->xabs, c->stream));
+    km::Geometry sub = c->g;
+    sub.n = m;
+    KM_HIP(km::launch_row_norm(c->X + (row0 + r) * dp, sub, c->xnorm + row0 + r, c->stream));
     KM_HIP(hipStreamSynchronize(c->stream));
   }
   return KM_OK;
@@ -370,6 +411,7 @@ int km_generate_blobs(km_ctx* c, int64_t n, int32_t d, int64_t global_row0, int3
   if (rc != KM_OK) return rc;
   KM_HIP(km::launch_gen_blobs(c->X, c->g, global_row0, n_centers, box, stddev, seed, c->stream));
   KM_HIP(km::launch_absmax(c->X, c->g.n * c->g.dp, c->xabs, c->stream));
+  KM_HIP(km::launch_row_norm(c->X, c->g, c->xnorm, c->stream));
   KM_HIP(hipStreamSynchronize(c->stream));
   return KM_OK;
 }
@@ -426,6 +468,9 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
     KM_HIP(hipMalloc(&c->Clo, sizeof(_Float16) * kp * dp));
     KM_HIP(hipMalloc(&c->cn2, sizeof(float) * kp));
     KM_HIP(hipMalloc(&c->cn2s, sizeof(float) * kp));
+    KM_HIP(hipMalloc(&c->ChiF, sizeof(_Float16) * kp * dp));
+    KM_HIP(hipMalloc(&c->CloF, sizeof(_Float16) * kp * dp));
+    KM_HIP(hipMalloc(&c->bnd, sizeof(float) * 4));
     KM_HIP(hipMalloc(&c->cmax, sizeof(float)));
     KM_HIP(hipMalloc(&c->cabs, sizeof(float)));
     KM_HIP(hipMalloc(&c->stats_own, sizeof(double) * (size_t)k * (d + 1)));
@@ -442,6 +487,7 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
       c->path = 2;
     else
       c->path = 0;
+    c->fused = (c->path == 2) && km::fused_path_ok(c->g) && !fused_disabled();
   }
   KM_HIP(hipMemcpyAsync(c->C64_cur, C, sizeof(double) * k * d, hipMemcpyHostToDevice, c->stream));
   int rc = prep(c);

@@ -7,7 +7,7 @@ for f in sorted(glob.glob(f"{root}/pmc*/run_counter_collection.csv")):
         kn = r["Kernel_Name"].split("(")[0][-40:]
         agg[kn][r["Counter_Name"]].append((r["Dispatch_Id"], float(r["Counter_Value"])))
 for kn, d in agg.items():
-    if not any(s in kn for s in ("assign", "stats", "rerank", "fullscan")):
+    if not any(s in kn for s in ("assign", "stats", "rerank", "fullscan", "fused")):
         continue
     out = {}
     for c, vals in d.items():
