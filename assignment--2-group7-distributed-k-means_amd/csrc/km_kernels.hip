@@ -782,7 +782,7 @@ __device__ __forceinline__ void perm_halves(uint32_t v, uint32_t& lo, uint32_t& 
 
 // ABL (diagnostic builds, KM_ABLATE=1..4, c3 shape only; results wrong):
 // 1 = no key updates, 2 = no MFMAs, 3 = no LDS sums, 4 = no merge / queue,
-// 5 = MFMAs + conversion + loads only
+// 5 = MFMAs + conversion + loads only, 6 = as 5 with L2-resident rows
 template <int NS, int NB, bool STATS, int ABL = 0>
 __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   constexpr int DP = 16 * NS;
@@ -825,7 +825,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   const float4* cnl = reinterpret_cast<const float4*>(sCn + 4 * h);  // + 8 blk + 2 g4
 
   auto load_tile = [&](int64_t tile, float4 (&xq)[NS][2], float& xnq) {
-    const int64_t row = tile * 32 + r;
+    const int64_t row = (ABL == 6 ? (tile & 7) : tile) * 32 + r;
     const int64_t rr = row < n ? row : (n - 1);
     const float* xr = A.X + rr * DP + 8 * h;
 #pragma unroll
@@ -892,7 +892,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
     // register reg holds centroid j = 32 blk + 4h + (reg & 3) + 8 (reg >> 2);
     // chain reg & 3 keeps the top three keys (score | j >> 2)
     auto keys_block = [&](const f32x16& acc, int blk) {
-      if constexpr (ABL == 1 || ABL == 5) {
+      if constexpr (ABL == 1 || ABL == 5 || ABL == 6) {
         a1[blk & 3] = fminf(a1[blk & 3], acc[0] + acc[15]);
         asm volatile("" ::"v"(acc));
         return;
@@ -929,7 +929,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
     }
     keys_block(accs[(NB - 1) & 1], NB - 1);
 
-    if constexpr (ABL == 5) {
+    if constexpr (ABL == 5 || ABL == 6) {
       const int lab = (int)(__float_as_uint(a1[0] + a1[1] + a1[2] + a1[3] + xn) & 255u) % A.k;
       if (h == 0 && valid) A.labels[row] = lab;
       return;
@@ -1160,12 +1160,13 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
     break;
   {
     static const char* abl = getenv("KM_ABLATE");
-    if (abl && ns == 4 && nb == 8 && with_stats && abl[0] >= '1' && abl[0] <= '5') {
+    if (abl && ns == 4 && nb == 8 && with_stats && abl[0] >= '1' && abl[0] <= '6') {
       switch (abl[0]) {
         case '1': hipLaunchKernelGGL((k_fused<4, 8, true, 1>), dim3(nbk), dim3(256), lds, s, a); break;
         case '2': hipLaunchKernelGGL((k_fused<4, 8, true, 2>), dim3(nbk), dim3(256), lds, s, a); break;
         case '3': hipLaunchKernelGGL((k_fused<4, 8, true, 3>), dim3(nbk), dim3(256), lds, s, a); break;
         case '5': hipLaunchKernelGGL((k_fused<4, 8, true, 5>), dim3(nbk), dim3(256), lds, s, a); break;
+        case '6': hipLaunchKernelGGL((k_fused<4, 8, true, 6>), dim3(nbk), dim3(256), lds, s, a); break;
         default: hipLaunchKernelGGL((k_fused<4, 8, true, 4>), dim3(nbk), dim3(256), lds, s, a); break;
       }
       return hipGetLastError();
