@@ -753,6 +753,32 @@ hipError_t launch_absmax(const float* X, int64_t nfloats, float* out, hipStream_
 // added by the resolver kernels, counts by k_count over the final labels.
 // The table is flushed with one float64 atomic per non-zero entry.
 // ---------------------------------------------------------------------------
+
+// min / max as v_med3 (no NaN-canonicalising v_max in front, unlike fminf)
+__device__ __forceinline__ float kmin(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, -FLT_MAX); }
+__device__ __forceinline__ float kmax(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, FLT_MAX); }
+
+// Merge two sorted key triples (K1<=K2<=K3 with indices P1,P2 of the first
+// two; likewise Q, R): the smallest three values and the indices of the
+// smallest two.  Ties keep the K side (deterministic in both lane halves).
+__device__ __forceinline__ void merge3(float& K1, float& K2, float& K3, uint32_t& P1, uint32_t& P2, float Q1,
+                                       float Q2, float Q3, uint32_t R1, uint32_t R2) {
+  const bool tk = K1 <= Q1;
+  const float sa = tk ? K2 : K1;  // candidates for the second
+  const float sb = tk ? Q1 : Q2;
+  const uint32_t ia = tk ? P2 : P1;
+  const uint32_t ib = tk ? R1 : R2;
+  const float n3 = kmin(kmin(K3, Q3), kmin(kmax(K1, Q2), kmax(K2, Q1)));
+  const float n1 = tk ? K1 : Q1;
+  const uint32_t q1 = tk ? P1 : R1;
+  const bool ta = sa <= sb;
+  K2 = ta ? sa : sb;
+  P2 = ta ? ia : ib;
+  K1 = n1;
+  P1 = q1;
+  K3 = n3;
+}
+
 struct FusedArgs {
   const float* X;
   const float* xnorm;  // per-row upper bound of ||x|| (unscaled)
@@ -851,7 +877,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
         const float xs = xv[e] * s;
         const _Float16 hi = (_Float16)xs;
         bh[t][e] = hi;
-        bl[t][e] = (_Float16)(xs - (float)hi);
+        bl[t][e] = (_Float16)__builtin_fmaf((float)hi, -1.0f, xs);  // v_fma_mix{lo,hi}_f16
       }
     }
     float a1[4], a2[4], a3[4];
@@ -949,37 +975,31 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       }
       return;
     }
-    // lane-local top-3 values and best two full indices over the kept keys
-    // (a chain's third never enters the top two)
-    float k1 = FLT_MAX, k2 = FLT_MAX, k3 = FLT_MAX;
-    uint32_t p1 = 0, p2 = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      top3p_insert(k1, k2, k3, p1, p2, a1[c], ((__float_as_uint(a1[c]) & maskq) << 2) | (uint32_t)c);
-      top3p_insert(k1, k2, k3, p1, p2, a2[c], ((__float_as_uint(a2[c]) & maskq) << 2) | (uint32_t)c);
-      top3p_insert(k1, k2, k3, p1, p2, a3[c], 0u);
+    // top-3 values and best two full indices: chains merged pairwise, then
+    // the two lane halves (disjoint centroid rows of the same point)
+    auto pidx = [&](float key, int c) { return ((__float_as_uint(key) & maskq) << 2) | (uint32_t)c; };
+    float k1 = a1[0], k2 = a2[0], k3 = a3[0];
+    uint32_t p1 = pidx(a1[0], 0), p2 = pidx(a2[0], 0);
+    {
+      float m1 = a1[2], m2 = a2[2], m3 = a3[2];
+      uint32_t q1 = pidx(a1[2], 2), q2 = pidx(a2[2], 2);
+      merge3(k1, k2, k3, p1, p2, a1[1], a2[1], a3[1], pidx(a1[1], 1), pidx(a2[1], 1));
+      merge3(m1, m2, m3, q1, q2, a1[3], a2[3], a3[3], pidx(a1[3], 3), pidx(a2[3], 3));
+      merge3(k1, k2, k3, p1, p2, m1, m2, m3, q1, q2);
     }
-    {  // merge the two lane halves (disjoint centroid rows of the same point)
+    {
       uint32_t K1, Q1, K2, Q2, K3, Q3, P1, R1, P2, R2;
       perm_halves(__float_as_uint(k1), K1, Q1);
       perm_halves(__float_as_uint(k2), K2, Q2);
       perm_halves(__float_as_uint(k3), K3, Q3);
       perm_halves(p1, P1, R1);
       perm_halves(p2, P2, R2);
-      const float fK1 = __uint_as_float(K1), fQ1 = __uint_as_float(Q1);
-      const float fK2 = __uint_as_float(K2), fQ2 = __uint_as_float(Q2);
-      const float fK3 = __uint_as_float(K3), fQ3 = __uint_as_float(Q3);
-      const bool takeK = fK1 <= fQ1;
-      k1 = takeK ? fK1 : fQ1;
-      p1 = takeK ? P1 : R1;
-      const float sa = takeK ? fK2 : fK1;   // candidates for the second
-      const float sb = takeK ? fQ1 : fQ2;
-      const uint32_t ia = takeK ? P2 : P1;
-      const uint32_t ib = takeK ? R1 : R2;
-      const bool ta = sa <= sb;
-      k2 = ta ? sa : sb;
-      p2 = ta ? ia : ib;
-      k3 = fminf(fminf(fK3, fQ3), fminf(fmaxf(fK1, fQ2), fmaxf(fK2, fQ1)));
+      k1 = __uint_as_float(K1);
+      k2 = __uint_as_float(K2);
+      k3 = __uint_as_float(K3);
+      p1 = P1;
+      p2 = P2;
+      merge3(k1, k2, k3, p1, p2, __uint_as_float(Q1), __uint_as_float(Q2), __uint_as_float(Q3), R1, R2);
     }
     // every candidate other than p1, p2 is >= k3 (a chain drops only keys
     // above its kept third)
@@ -1217,10 +1237,60 @@ hipError_t launch_count(const int32_t* labels, const Geometry& g, double* stats,
 //                they fit (read from L2 otherwise).
 // Walks the per-wave queue segments written by k_assign_mfma.
 // ---------------------------------------------------------------------------
+// Exclusive prefix over the per-segment queue counts (word `which` of each
+// count pair) into LDS pre[0..nseg]; blockDim.x == 1024.
+__device__ void block_prefix(const uint32_t* __restrict__ qcount, int which, uint32_t nseg,
+                             uint32_t* __restrict__ pre) {
+  __shared__ uint32_t wsum[16];
+  const uint32_t t = threadIdx.x;
+  const uint32_t chunk = (nseg + 1023u) / 1024u;
+  const uint32_t b0 = t * chunk;
+  uint32_t v = 0;
+  for (uint32_t i = 0; i < chunk; ++i)
+    if (b0 + i < nseg) v += qcount[2 * (b0 + i) + which];
+  const int lane = t & 63, w = t >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int i = 0; i < w; ++i) base += wsum[i];
+  uint32_t run = base + inc - v;  // exclusive prefix of this thread's chunk
+  for (uint32_t i = 0; i < chunk; ++i)
+    if (b0 + i < nseg) {
+      pre[b0 + i] = run;
+      run += qcount[2 * (b0 + i) + which];
+    }
+  if (t == 1023) {
+    uint32_t tot = 0;
+    for (int i = 0; i < 16; ++i) tot += wsum[i];
+    pre[nseg] = tot;
+  }
+  __syncthreads();
+}
+
+// segment holding global entry g: the last sg with pre[sg] <= g
+__device__ __forceinline__ uint32_t find_segment(const uint32_t* __restrict__ pre, uint32_t nseg, uint32_t g) {
+  uint32_t lo = 0, hi = nseg;  // pre[lo] <= g < pre[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pre[mid] <= g)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
 // With stats != nullptr the resolved points' rows are added to the partial
 // sums (the fused kernel leaves every queued point to the resolvers): into an
 // LDS table [f][j] flushed at the end when it fits (tab_kp > 0), else with
-// global float64 atomics.
+// global float64 atomics.  The entries of all segments are spread over all
+// waves of the grid (16 lanes per entry, 4 entries per wave-iteration).
 __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, int dp, int d, int k,
                                                   const double* __restrict__ C64, const QEntry* __restrict__ queue,
                                                   const uint32_t* __restrict__ qcount, QLayout ql,
@@ -1228,25 +1298,25 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
                                                   int tab_kp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* tab = reinterpret_cast<double*>(smem);
-  if (stats && tab_kp) {
+  uint32_t* pre = reinterpret_cast<uint32_t*>(smem + (stats && tab_kp ? (size_t)d * tab_kp * 8 : 0));
+  if (stats && tab_kp)
     for (int i = threadIdx.x; i < d * tab_kp; i += blockDim.x) tab[i] = 0.0;
-    __syncthreads();
-  }
+  block_prefix(qcount, 0, ql.nwaves, pre);
+  const uint32_t total = pre[ql.nwaves];
   const int lane = threadIdx.x & 63;
   const int sub = lane >> 4;   // entry slot in the wave
   const int m = lane & 15;     // features 4m..4m+3 (+64t)
   const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
-  // every assign wave wrote about the same number of entries: one resolve
-  // wave per segment (grid-stride), 4 entries per wave-iteration
-  for (uint32_t sg = gw; sg < ql.nwaves; sg += nw) {
-    const uint32_t cnt = qcount[2 * sg];
-    const QEntry* qs = queue + (size_t)sg * ql.seg;
-    for (uint32_t e0 = 0; e0 < cnt; e0 += 4) {
-      const uint32_t e = e0 + (uint32_t)sub;
-      const bool have = e < cnt;
+  for (uint32_t g0 = gw * 4; g0 < total; g0 += nw * 4) {
+    {
+      const uint32_t g = g0 + (uint32_t)sub;
+      const bool have = g < total;
       QEntry q{0, 0, 0, 0};
-      if (have) q = qs[e];
+      if (have) {
+        const uint32_t sg = find_segment(pre, ql.nwaves, g);
+        q = queue[(size_t)sg * ql.seg + (g - pre[sg])];
+      }
       const bool ok = have && q.i1 < (uint32_t)k && q.i2 < (uint32_t)k;
       double s1 = 0.0, s2 = 0.0;
       if (ok) {
@@ -1330,7 +1400,6 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
   }
 }
 
-static constexpr int FULLSCAN_LDS = 152 * 1024;
 
 __global__ __launch_bounds__(1024) void k_fullscan(const float* __restrict__ X, int dp, int d, int k,
                                                    const double* __restrict__ C64T, const QEntry* __restrict__ queue,
@@ -1339,25 +1408,23 @@ __global__ __launch_bounds__(1024) void k_fullscan(const float* __restrict__ X, 
                                                    double* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sCT = reinterpret_cast<double*>(smem);
-  if (use_lds) {
+  uint32_t* pre = reinterpret_cast<uint32_t*>(smem + (use_lds ? (size_t)k * d * 8 : 0));
+  if (use_lds)
     for (int i = threadIdx.x; i < k * d; i += blockDim.x) sCT[i] = C64T[i];
-    __syncthreads();
-  }
+  block_prefix(qcount, 1, ql.nwaves, pre);
+  const uint32_t total = pre[ql.nwaves];
   const double* CT = use_lds ? sCT : C64T;
   const int lane = threadIdx.x & 63;
   const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
-  // one wave per segment (grid-stride); each segment's full-scan entries sit
-  // at its back.  The point's row is held one feature per lane and broadcast
-  // with v_readlane; lanes run over centroids (C64T rows are contiguous in j).
-  // entries of all segments are spread over all waves (entry e of segment
-  // sg goes to wave (e + 7919 sg) mod nw): segments hold a few entries each,
-  // and a wave per segment would leave most waves idle with the dependent
-  // queue -> row -> data loads exposed)
-  for (uint32_t sg = 0; sg < ql.nwaves; ++sg) {
-    const uint32_t cnt = qcount[2 * sg + 1];
-    const uint32_t first = (gw + nw - (uint32_t)(((uint64_t)sg * 7919u) % nw)) % nw;
-    for (uint32_t e = first; e < cnt; e += nw) {
+  // one wave per entry, entries of all segments spread over all waves; the
+  // point's row is held one feature per lane and broadcast with v_readlane;
+  // lanes run over centroids (C64T rows are contiguous in j).  Full-scan
+  // entries sit at the back of each segment.
+  for (uint32_t g = gw; g < total; g += nw) {
+    {
+      const uint32_t sg = find_segment(pre, ql.nwaves, g);
+      const uint32_t e = g - pre[sg];
       const QEntry* qp = queue + (size_t)sg * ql.seg + (ql.seg - 1u - e);
       const uint32_t row = __builtin_amdgcn_readfirstlane(qp->row);
       const float* x = X + (size_t)row * dp;
@@ -1405,16 +1472,19 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
                           double* stats, int n_cu, hipStream_t s) {
   if (g.n == 0 || ql.nwaves == 0) return hipSuccess;
+  constexpr size_t LDS_MAX = 160 * 1024;
+  const size_t pre_bytes = ((size_t)ql.nwaves + 1) * 4;
+  if (pre_bytes > LDS_MAX / 2) return hipErrorInvalidValue;
   const size_t tab_bytes = (size_t)g.d * g.kp * 8;
-  const int tab_kp = (stats && tab_bytes <= FULLSCAN_LDS) ? g.kp : 0;
-  hipLaunchKernelGGL(k_rerank2, dim3(n_cu), dim3(1024), tab_kp ? tab_bytes : 0, s, X, g.dp, g.d, g.k, C64, queue,
-                     qcount, ql, labels, stats, tab_kp);
+  const int tab_kp = (stats && tab_bytes + pre_bytes <= LDS_MAX) ? g.kp : 0;
+  hipLaunchKernelGGL(k_rerank2, dim3(n_cu), dim3(1024), (tab_kp ? tab_bytes : 0) + pre_bytes, s, X, g.dp, g.d, g.k,
+                     C64, queue, qcount, ql, labels, stats, tab_kp);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t bytes = (size_t)g.k * g.d * 8;
-  const int use_lds = bytes <= FULLSCAN_LDS ? 1 : 0;
-  hipLaunchKernelGGL(k_fullscan, dim3(n_cu), dim3(1024), use_lds ? bytes : 0, s, X, g.dp, g.d, g.k, C64T, queue,
-                     qcount, ql, labels, use_lds, stats);
+  const int use_lds = bytes + pre_bytes <= LDS_MAX ? 1 : 0;
+  hipLaunchKernelGGL(k_fullscan, dim3(n_cu), dim3(1024), (use_lds ? bytes : 0) + pre_bytes, s, X, g.dp, g.d, g.k,
+                     C64T, queue, qcount, ql, labels, use_lds, stats);
   return hipGetLastError();
 }
 
