@@ -74,6 +74,7 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
 // lo image + float64 sum table in LDS; decided points summed here, queued
 // points by launch_resolve(stats), sizes by launch_count.
 bool fused_path_ok(const Geometry& g);
+void dump_fused_stamps();  // diagnostic (KM_ABLATE=7)
 hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, const _Float16* Chi,
                         const _Float16* Clo, uint4* ChiF, uint4* CloF, const float* cn2s, const float* bnd,
                         const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,

@@ -11,6 +11,7 @@
 #include "km_internal.h"
 
 #include <float.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 namespace km {
@@ -779,6 +780,9 @@ __device__ __forceinline__ void merge3(float& K1, float& K2, float& K3, uint32_t
   K3 = n3;
 }
 
+// diagnostic stamp accumulators (ABL == 7 builds only): per-phase cycles
+__device__ unsigned long long g_stamp[8];
+
 struct FusedArgs {
   const float* X;
   const float* xnorm;  // per-row upper bound of ||x|| (unscaled)
@@ -862,6 +866,9 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
     xnq = A.xnorm[rr];
   };
 
+  unsigned long long st_acc[5] = {0, 0, 0, 0, 0};
+  unsigned long long st_last = 0;
+  if constexpr (ABL == 7) st_last = __builtin_amdgcn_s_memtime();
   auto process_tile = [&](int64_t tile, const float4 (&xc)[NS][2], float xn) {
     const int64_t row = tile * 32 + r;
     const bool valid = row < n;
@@ -879,6 +886,13 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
         bh[t][e] = hi;
         bl[t][e] = (_Float16)__builtin_fmaf((float)hi, -1.0f, xs);  // v_fma_mix{lo,hi}_f16
       }
+    }
+    if constexpr (ABL == 7) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long tnow = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      st_acc[0] += tnow - st_last;
+      st_last = tnow;
     }
     float a1[4], a2[4], a3[4];
 #pragma unroll
@@ -954,6 +968,13 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       __builtin_amdgcn_sched_barrier(0);
     }
     keys_block(accs[(NB - 1) & 1], NB - 1);
+    if constexpr (ABL == 7) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long tnow = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      st_acc[1] += tnow - st_last;
+      st_last = tnow;
+    }
 
     if constexpr (ABL == 5 || ABL == 6) {
       const int lab = (int)(__float_as_uint(a1[0] + a1[1] + a1[2] + a1[3] + xn) & 255u) % A.k;
@@ -1011,6 +1032,13 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       kind = 2;
     else if (!(k2 - k1 > thr2))
       kind = 1;
+    if constexpr (ABL == 7) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long tnow = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      st_acc[2] += tnow - st_last;
+      st_last = tnow;
+    }
     const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
     if (h == 0 && valid) A.labels[row] = lab;
     const bool enq = (h == 0) && valid && (kind != 0);
@@ -1032,6 +1060,13 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       qn += (uint32_t)__popcll(m1);
       qf += (uint32_t)__popcll(m2);
     }
+    if constexpr (ABL == 7) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long tnow = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      st_acc[3] += tnow - st_last;
+      st_last = tnow;
+    }
     if constexpr (STATS && ABL != 3) {
       if (valid && kind == 0) {
         double* tp = tab + (size_t)(8 * h) * KP + lab;
@@ -1044,7 +1079,14 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
         }
       }
     }
-    };
+    if constexpr (ABL == 7) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long tnow = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      st_acc[4] += tnow - st_last;
+      st_last = tnow;
+    }
+  };
 
   // tiles of this wave, two register buffers: the next tile's rows are in
   // flight while this one is processed
@@ -1062,6 +1104,10 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   if (lane == 0) {
     A.qcount[2 * gw] = qn;
     A.qcount[2 * gw + 1] = qf;
+  }
+  if constexpr (ABL == 7) {
+    if (lane == 0)
+      for (int i = 0; i < 5; ++i) atomicAdd(&g_stamp[i], st_acc[i]);
   }
   if constexpr (STATS) {
     __syncthreads();
@@ -1134,6 +1180,24 @@ __global__ __launch_bounds__(1024) void k_count(const int32_t* __restrict__ labe
     if (hist[i]) atomicAdd(stats + (size_t)i * (d + 1) + d, (double)hist[i]);
 }
 
+// diagnostic: print and clear the ABL=7 phase stamps (cycles summed over waves)
+void dump_fused_stamps() {
+  unsigned long long v[8];
+  const hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_stamp), sizeof(v));
+  if (e != hipSuccess) {
+    fprintf(stderr, "[km stamps] read failed: %s\n", hipGetErrorString(e));
+    return;
+  }
+  unsigned long long tot = 0;
+  for (int i = 0; i < 5; ++i) tot += v[i];
+  fprintf(stderr, "[km stamps] total %llu\n", tot);
+  if (tot == 0) return;
+  fprintf(stderr, "[km stamps] split %.3f blocks %.3f merge %.3f queue %.3f sums %.3f (fractions)\n",
+          (double)v[0] / tot, (double)v[1] / tot, (double)v[2] / tot, (double)v[3] / tot, (double)v[4] / tot);
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z));
+}
+
 bool fused_path_ok(const Geometry& g) {
   const int ns = g.dp / 16, nb = g.kp / 32;
   if (g.dp % 16 || g.kp % 64) return false;
@@ -1180,12 +1244,13 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
     break;
   {
     static const char* abl = getenv("KM_ABLATE");
-    if (abl && ns == 4 && nb == 8 && with_stats && abl[0] >= '1' && abl[0] <= '6') {
+    if (abl && ns == 4 && nb == 8 && with_stats && abl[0] >= '1' && abl[0] <= '7') {
       switch (abl[0]) {
         case '1': hipLaunchKernelGGL((k_fused<4, 8, true, 1>), dim3(nbk), dim3(256), lds, s, a); break;
         case '2': hipLaunchKernelGGL((k_fused<4, 8, true, 2>), dim3(nbk), dim3(256), lds, s, a); break;
         case '3': hipLaunchKernelGGL((k_fused<4, 8, true, 3>), dim3(nbk), dim3(256), lds, s, a); break;
         case '5': hipLaunchKernelGGL((k_fused<4, 8, true, 5>), dim3(nbk), dim3(256), lds, s, a); break;
+        case '7': hipLaunchKernelGGL((k_fused<4, 8, true, 7>), dim3(nbk), dim3(256), lds, s, a); break;
         case '6': hipLaunchKernelGGL((k_fused<4, 8, true, 6>), dim3(nbk), dim3(256), lds, s, a); break;
         default: hipLaunchKernelGGL((k_fused<4, 8, true, 4>), dim3(nbk), dim3(256), lds, s, a); break;
       }

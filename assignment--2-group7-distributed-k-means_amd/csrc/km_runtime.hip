@@ -328,6 +328,10 @@ int km_sync(km_ctx* c) {
   KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
   KM_HIP(hipSetDevice(c->device));
   KM_HIP(hipStreamSynchronize(c->stream));
+  {
+    static const char* abl = getenv("KM_ABLATE");
+    if (abl && abl[0] == '7') km::dump_fused_stamps();
+  }
   return KM_OK;
 }
 

@@ -6,7 +6,7 @@
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-template <int NB, bool AGPR, int CHAINS>
+template <int NB, bool AGPR, int CHAINS, bool INDEP = false>
 __global__ __launch_bounds__(256, 1) void chain(const f16x8* img, float* out, int iters) {
   const int lane = threadIdx.x & 63;
   f16x8 A[NB][4];
@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256, 1) void chain(const f16x8* img, float* out, in
 #pragma unroll
       for (int c = 0; c < CHAINS; ++c)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[c][i] = sink;
+        for (int i = 0; i < 16; ++i) acc[c][i] = INDEP ? 0.0f : sink;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -40,20 +40,20 @@ __global__ __launch_bounds__(256, 1) void chain(const f16x8* img, float* out, in
           for (int c = 0; c < CHAINS; ++c)
             acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[b + c][t], bv[(t + rep) & 3], acc[c], 0, 0, 0);
 #pragma unroll
-      for (int c = 0; c < CHAINS; ++c) sink += acc[c][0] * 1e-30f;
+      for (int c = 0; c < CHAINS; ++c) sink = INDEP ? fmaxf(sink, acc[c][b & 15]) : sink + acc[c][0] * 1e-30f;
     }
   }
   out[blockIdx.x * blockDim.x + threadIdx.x] = sink;
 }
 
-template <int NB, bool AGPR, int CHAINS>
+template <int NB, bool AGPR, int CHAINS, bool INDEP = false>
 static void run(const f16x8* img, float* out, int n_cu, const char* name) {
   const int iters = 400;
   hipEvent_t a, b;
   (void)hipEventCreate(&a); (void)hipEventCreate(&b);
-  hipLaunchKernelGGL((chain<NB, AGPR, CHAINS>), dim3(n_cu), dim3(256), 0, 0, img, out, iters);
+  hipLaunchKernelGGL((chain<NB, AGPR, CHAINS, INDEP>), dim3(n_cu), dim3(256), 0, 0, img, out, iters);
   (void)hipEventRecord(a);
-  hipLaunchKernelGGL((chain<NB, AGPR, CHAINS>), dim3(n_cu), dim3(256), 0, 0, img, out, iters);
+  hipLaunchKernelGGL((chain<NB, AGPR, CHAINS, INDEP>), dim3(n_cu), dim3(256), 0, 0, img, out, iters);
   (void)hipEventRecord(b);
   (void)hipEventSynchronize(b);
   float ms; (void)hipEventElapsedTime(&ms, a, b);
@@ -73,5 +73,7 @@ int main() {
   run<8, false, 1>(img, out, n_cu, "VGPR A, 1 chain");
   run<8, false, 2>(img, out, n_cu, "VGPR A, 2 chains");
   run<4, false, 1>(img, out, n_cu, "VGPR A (4 blk), 1 chain");
+  run<8, true, 1, true>(img, out, n_cu, "AGPR A, indep blocks");
+  run<8, true, 2, true>(img, out, n_cu, "AGPR A, indep, 2 chains");
   return 0;
 }
