@@ -83,6 +83,12 @@ hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float
                                hipStream_t s);
 hipError_t launch_row_norm(const float* X, const Geometry& g, float* xnorm, hipStream_t s);
 hipError_t launch_count(const int32_t* labels, const Geometry& g, double* stats, int n_cu, hipStream_t s);
+// large k: counting sort of the labels + per-cluster float64 row sums (X read
+// once); scratch = sorted_stats_words(n, k) uint32 words
+bool stats_needs_sort(const Geometry& g);
+size_t sorted_stats_words(int64_t n, int k);
+hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t* labels, double* stats,
+                               uint32_t* scratch, int n_cu, hipStream_t s);
 hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels, double* stats, int n_cu,
                         hipStream_t s);
 hipError_t launch_update(const double* stats, const double* C64_old, const double* mu, const Geometry& g,

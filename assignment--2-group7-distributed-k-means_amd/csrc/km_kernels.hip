@@ -1656,6 +1656,195 @@ hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels
 }
 
 // ---------------------------------------------------------------------------
+// Partial statistics for large k (k (d+1) doubles beyond LDS: c4, c5).  The
+// range-tiled k_stats would re-read X once per LDS-sized cluster range (28x
+// at k=4096, d=128); instead the labels are counting-sorted (histogram ->
+// exclusive scan -> scatter of row ids) and each cluster's rows are summed in
+// float64 by one workgroup with plain stores (no atomics): X is read once,
+// as gathered whole rows.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_hist(const int32_t* __restrict__ labels, int64_t n, int k,
+                                               uint32_t* __restrict__ cnt) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
+  for (int i = threadIdx.x; i < k; i += blockDim.x) hist[i] = 0u;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int l = labels[i];
+    if ((unsigned)l < (unsigned)k) atomicAdd(hist + l, 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < k; i += blockDim.x)
+    if (hist[i]) atomicAdd(cnt + i, hist[i]);
+}
+
+// exclusive scan of cnt[k] into off[k] and cur[k] (scatter cursors); one block
+__global__ __launch_bounds__(1024) void k_scan(const uint32_t* __restrict__ cnt, int k, uint32_t* __restrict__ off,
+                                               uint32_t* __restrict__ cur) {
+  __shared__ uint32_t wsum[16];
+  const int t = threadIdx.x;
+  const int chunk = (k + 1023) / 1024;
+  const int b0 = t * chunk;
+  uint32_t v = 0;
+  for (int i = 0; i < chunk; ++i)
+    if (b0 + i < k) v += cnt[b0 + i];
+  const int lane = t & 63, w = t >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t run = inc - v;
+  for (int i = 0; i < w; ++i) run += wsum[i];
+  for (int i = 0; i < chunk; ++i)
+    if (b0 + i < k) {
+      off[b0 + i] = run;
+      cur[b0 + i] = run;
+      run += cnt[b0 + i];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_scatter(const int32_t* __restrict__ labels, int64_t n, int k,
+                                                 uint32_t* __restrict__ cur, uint32_t* __restrict__ perm,
+                                                 int32_t* __restrict__ slab) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int l = labels[i];
+    if ((unsigned)l < (unsigned)k) {
+      const uint32_t pos = atomicAdd(cur + l, 1u);
+      perm[pos] = (uint32_t)i;
+      slab[pos] = l;
+    }
+  }
+}
+
+// Segmented float64 sums over the label-sorted order: every wave takes an
+// equal contiguous range of sorted positions; a lane group of L = dp/4 lanes
+// owns one row per load (float4 per lane, 64/L rows per wave-instruction, U
+// instructions in flight) and keeps a running float64 sum while its rows stay
+// in one cluster, flushing it with global float64 atomics (contiguous 16 B
+// per lane) when the cluster changes and at the end.  Counts come from the
+// histogram.
+template <int L>  // lanes per row = dp / 4
+__global__ __launch_bounds__(256) void k_segsum(const float* __restrict__ X, int d, int64_t n,
+                                                const uint32_t* __restrict__ perm, const int32_t* __restrict__ slab,
+                                                double* __restrict__ stats) {
+  constexpr int P = 64 / L;  // rows per wave-instruction
+  constexpr int U = 4;       // instructions in flight
+  constexpr int DP = 4 * L;
+  const int lane = threadIdx.x & 63;
+  const int q = lane / L;
+  const int m = lane % L;
+  if (q >= P) return;  // dp = 48, 96, 192: the lanes past the last whole row idle (no barriers here)
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t per = (n + nw - 1) / nw;
+  const int64_t p0 = gw * per;
+  const int64_t p1 = p0 + per < n ? p0 + per : n;
+  const int d1 = d + 1;
+  int cur = -1;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  auto flush = [&]() {
+    if (cur >= 0) {
+      double* o = stats + (size_t)cur * d1 + 4 * m;
+      if (4 * m + 0 < d) atomicAdd(o + 0, a0);
+      if (4 * m + 1 < d) atomicAdd(o + 1, a1);
+      if (4 * m + 2 < d) atomicAdd(o + 2, a2);
+      if (4 * m + 3 < d) atomicAdd(o + 3, a3);
+    }
+    a0 = a1 = a2 = a3 = 0.0;
+  };
+  for (int64_t base = p0; base < p1; base += P * U) {
+    float4 v[U];
+    int lb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t pos = base + u * P + q;
+      if (pos < p1) {
+        const uint32_t row = perm[pos];
+        lb[u] = slab[pos];
+        v[u] = *reinterpret_cast<const float4*>(X + (size_t)row * DP + 4 * m);
+      } else {
+        lb[u] = -1;
+        v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (lb[u] < 0) continue;
+      if (lb[u] != cur) {
+        flush();
+        cur = lb[u];
+      }
+      a0 += (double)v[u].x;
+      a1 += (double)v[u].y;
+      a2 += (double)v[u].z;
+      a3 += (double)v[u].w;
+    }
+  }
+  flush();
+}
+
+// counts of the histogram into the count column
+__global__ void k_put_counts(const uint32_t* __restrict__ cnt, int k, int d, double* __restrict__ stats) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < k) stats[(size_t)j * (d + 1) + d] = (double)cnt[j];
+}
+
+size_t sorted_stats_words(int64_t n, int k) { return 2 * (size_t)n + 3 * (size_t)k + 64; }
+
+// the range-tiled k_stats reads X once per LDS-sized cluster range; from three
+// ranges on, the sort (one gathered read of X plus ~5 bytes per row of
+// label/permutation traffic, and cursor atomics that contend when k is small)
+// is cheaper
+bool stats_needs_sort(const Geometry& g) {
+  const size_t kr = (size_t)STATS_LDS / ((size_t)(g.dp + 1) * 8);
+  return kr == 0 || ((size_t)g.k + kr - 1) / kr >= 3;
+}
+
+hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t* labels, double* stats,
+                               uint32_t* scratch, int n_cu, hipStream_t s) {
+  if (g.n == 0) return hipSuccess;
+  if (g.dp > 256) return hipErrorInvalidValue;
+  uint32_t* cnt = scratch;
+  uint32_t* off = cnt + g.k;
+  uint32_t* cur = off + g.k;
+  uint32_t* perm = cur + g.k;
+  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint32_t) * g.k, s);
+  if (e != hipSuccess) return e;
+  int64_t hb = (g.n + 1023) / 1024;
+  if (hb > n_cu * 2) hb = n_cu * 2;
+  const size_t hist_lds = (size_t)g.k * 4;
+  if (hist_lds > 64 * 1024) return hipErrorInvalidValue;  // k <= 16384
+  hipLaunchKernelGGL(k_hist, dim3((unsigned)hb), dim3(1024), hist_lds, s, labels, g.n, g.k, cnt);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, cnt, g.k, off, cur);
+  int64_t sb = (g.n + 255) / 256;
+  if (sb > n_cu * 16) sb = n_cu * 16;
+  int32_t* slab = reinterpret_cast<int32_t*>(perm + g.n);
+  hipLaunchKernelGGL(k_scatter, dim3((unsigned)sb), dim3(256), 0, s, labels, g.n, g.k, cur, perm, slab);
+  hipLaunchKernelGGL(k_put_counts, dim3((g.k + 255) / 256), dim3(256), 0, s, cnt, g.k, g.d, stats);
+  // every label is in [0, k) (the assign kernels map non-finite rows to 0),
+  // so all n sorted positions are written
+  const int64_t nsorted = g.n;
+  int64_t wb = (int64_t)n_cu * 8;
+  const unsigned grid = (unsigned)wb;
+  switch (g.dp / 4) {
+    case 4: hipLaunchKernelGGL(k_segsum<4>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
+    case 8: hipLaunchKernelGGL(k_segsum<8>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
+    case 12: hipLaunchKernelGGL(k_segsum<12>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
+    case 16: hipLaunchKernelGGL(k_segsum<16>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
+    case 24: hipLaunchKernelGGL(k_segsum<24>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
+    case 32: hipLaunchKernelGGL(k_segsum<32>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
+    case 48: hipLaunchKernelGGL(k_segsum<48>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
+    case 64: hipLaunchKernelGGL(k_segsum<64>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Centroid update (kmeans_spark.py:176-206 + 278-294): new = sum / count,
 // empties keep the old centroid (host replaces them, L191-204), per-cluster
 // squared shift, SSE via the closed form

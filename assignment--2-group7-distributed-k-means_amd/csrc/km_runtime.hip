@@ -101,6 +101,8 @@ struct km_ctx {
   uint4* ChiF = nullptr;     // fragment-linear hi / lo images (fused kernel)
   uint4* CloF = nullptr;
   float* bnd = nullptr;      // screening-bound constants
+  uint32_t* sort_scratch = nullptr;  // label sort of the large-k statistics
+  size_t sort_words = 0;
   double* stats_own = nullptr;
   double* stats = nullptr;
   double* work = nullptr;
@@ -185,6 +187,8 @@ void free_data(km_ctx* c) {
   dfree(c->moments);
   dfree(c->xabs);
   dfree(c->xnorm);
+  dfree(c->sort_scratch);
+  c->sort_words = 0;
   dfree(c->mu);
   dfree(c->sse_base);
   dfree(c->idx_scratch);
@@ -251,7 +255,17 @@ int run_assign(km_ctx* c, bool with_stats) {
   }
   if (with_stats) {
     ProfScope ps(c, KM_K_STATS);
-    KM_HIP(km::launch_stats(c->X, g, c->labels, c->stats, c->n_cu, c->stream));
+    if (km::stats_needs_sort(g)) {
+      const size_t words = km::sorted_stats_words(g.n, g.k);
+      if (words > c->sort_words) {
+        dfree(c->sort_scratch);
+        KM_HIP(hipMalloc(&c->sort_scratch, sizeof(uint32_t) * words));
+        c->sort_words = words;
+      }
+      KM_HIP(km::launch_stats_sorted(c->X, g, c->labels, c->stats, c->sort_scratch, c->n_cu, c->stream));
+    } else {
+      KM_HIP(km::launch_stats(c->X, g, c->labels, c->stats, c->n_cu, c->stream));
+    }
   }
   return KM_OK;
 }
