@@ -184,5 +184,11 @@ class HipEngine:
 
 
 def make_engine(comm, device: Optional[int] = None) -> HipEngine:
-    dev = comm.local_rank if device is None else device
+    """One engine per rank on GPU ``LOCAL_RANK`` (taken modulo the visible
+    devices, so several ranks can share one GPU when rehearsing)."""
+    if device is None:
+        n = _lib.device_count()
+        dev = comm.local_rank % n if n > 0 else comm.local_rank
+    else:
+        dev = device
     return HipEngine(dev, distributed=comm.world > 1)

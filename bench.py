@@ -59,8 +59,13 @@ def init_dist(args):
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        dev = local % max(torch.cuda.device_count(), 1)   # == local on a full node
+        torch.cuda.set_device(dev)
+        backend = os.environ.get("KM_DIST_BACKEND", "nccl")  # nccl == RCCL; gloo only to rehearse on one GPU
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -125,7 +130,8 @@ def main():
     dt = float(comm.allreduce_np(np.array([t1 - t0])).max()) if world == 1 else None
     if world > 1:
         import torch.distributed as dist
-        t = torch.tensor([t1 - t0], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([t1 - t0], dtype=torch.float64,
+                         device=f"cuda:{torch.cuda.current_device()}" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 

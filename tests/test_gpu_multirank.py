@@ -1,0 +1,89 @@
+"""Multi-rank path on the GPU: two processes (torch.distributed over gloo, both
+on cuda:0 because the test box has one GPU) run the real HIP engine on their
+row shards and exchange the [k][d+1] float64 statistics with the same
+stream-ordered all-reduce the RCCL path uses (engine.run_collective).  Results
+must match the reference's golden vectors like the single-rank run does:
+the shard-invariance the 1..8 GPU scaling bench relies on
+(kmeans_spark.py:169-173 -> one all-reduce per iteration)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, name, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import contextlib
+        import io
+        import kmeans_amd as ka
+        from conftest import load_golden
+        g = load_golden(name)
+        init = g["init"]
+
+        class Pinned(ka.KMeans):
+            def _initialize_centroids(self, run):
+                return init.copy()
+
+            def _empty_seed(self):
+                return int(g["time_seed"])
+
+        sc = ka.LocalContext()
+        rdd = sc.parallelize(g["X"], int(g["slices"]))
+        km = Pinned(k=int(g["k"]), max_iter=int(g["max_iter"]), tolerance=float(g["tol"]), seed=int(g["seed"]),
+                    compute_sse=bool(g["sse"]))
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            km.fit(rdd, sc)
+        labels = np.array(km.predict(rdd, sc).collect())
+        assert km._runner.engine.distributed
+        q.put((rank, km.centroids, km.sse_history, labels, buf.getvalue(), km._runner.pl.n_local))
+    except Exception as e:  # surface the failure in the parent
+        q.put((rank, repr(e), None, None, None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["test_a", "empty", "c3_small"])
+def test_two_ranks_on_gpu_match_reference(golden, name):
+    import torch.multiprocessing as mp
+    g = golden(name)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, name, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=110) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0, res
+    assert sum(r[5] for r in res) == len(g["X"])  # the shards partition the rows
+    for rank, C, sse, labels, out, _ in res:
+        np.testing.assert_allclose(C, g["centroids"], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(sse, g["sse_history"], rtol=1e-9)
+        np.testing.assert_array_equal(labels, g["labels"])
+    assert res[0][4] and not res[1][4]  # only rank 0 logs
