@@ -812,7 +812,8 @@ __device__ __forceinline__ void perm_halves(uint32_t v, uint32_t& lo, uint32_t& 
 
 // ABL (diagnostic builds, KM_ABLATE=1..4, c3 shape only; results wrong):
 // 1 = no key updates, 2 = no MFMAs, 3 = no LDS sums, 4 = no merge / queue,
-// 5 = MFMAs + conversion + loads only, 6 = as 5 with L2-resident rows
+// 5 = MFMAs + conversion + loads only, 6 = as 5 with L2-resident rows,
+// 7 = full kernel with s_memtime phase stamps, 8 = full kernel, compiler schedule
 template <int NS, int NB, bool STATS, int ABL = 0>
 __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   constexpr int DP = 16 * NS;
@@ -957,6 +958,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       accs[blk & 1] = mfma_block(cin, blk);
       keys_block(accs[(blk - 1) & 1], blk - 1);
       // MFMA, next block's init reads, MFMA, then (VALU x m, MFMA) pairs
+      if constexpr (ABL == 8) continue;  // diagnostic: compiler's own schedule
       __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
       __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
@@ -1244,13 +1246,14 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
     break;
   {
     static const char* abl = getenv("KM_ABLATE");
-    if (abl && ns == 4 && nb == 8 && with_stats && abl[0] >= '1' && abl[0] <= '7') {
+    if (abl && ns == 4 && nb == 8 && with_stats && abl[0] >= '1' && abl[0] <= '8') {
       switch (abl[0]) {
         case '1': hipLaunchKernelGGL((k_fused<4, 8, true, 1>), dim3(nbk), dim3(256), lds, s, a); break;
         case '2': hipLaunchKernelGGL((k_fused<4, 8, true, 2>), dim3(nbk), dim3(256), lds, s, a); break;
         case '3': hipLaunchKernelGGL((k_fused<4, 8, true, 3>), dim3(nbk), dim3(256), lds, s, a); break;
         case '5': hipLaunchKernelGGL((k_fused<4, 8, true, 5>), dim3(nbk), dim3(256), lds, s, a); break;
         case '7': hipLaunchKernelGGL((k_fused<4, 8, true, 7>), dim3(nbk), dim3(256), lds, s, a); break;
+        case '8': hipLaunchKernelGGL((k_fused<4, 8, true, 8>), dim3(nbk), dim3(256), lds, s, a); break;
         case '6': hipLaunchKernelGGL((k_fused<4, 8, true, 6>), dim3(nbk), dim3(256), lds, s, a); break;
         default: hipLaunchKernelGGL((k_fused<4, 8, true, 4>), dim3(nbk), dim3(256), lds, s, a); break;
       }
