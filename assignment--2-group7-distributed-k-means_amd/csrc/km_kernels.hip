@@ -1152,17 +1152,42 @@ __global__ void k_bound_consts(const float* __restrict__ cmax, const float* __re
   bnd[1] = 1.5f * ((float)(3 * dp + 5) * U24 * cm * cm + 2.0f * U24 * sq * cm);
 }
 
-// upper bound of ||x|| per row (float64 sum, rounded up)
-__global__ __launch_bounds__(256) void k_row_norm(const float* __restrict__ X, int64_t n, int dp,
-                                                  float* __restrict__ xnorm) {
-  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < n;
-       row += (int64_t)gridDim.x * blockDim.x) {
-    double s = 0.0;
-    for (int f = 0; f < dp; ++f) {
-      const double v = X[row * dp + f];
-      s = fma(v, v, s);
+// upper bound of ||x|| per row (float64 sum, rounded up): L = dp/4 lanes per
+// row read float4s (coalesced), partial sums combined with xor-shuffles
+template <int L>
+__global__ __launch_bounds__(256) void k_row_norm(const float* __restrict__ X, int64_t n, float* __restrict__ xnorm) {
+  constexpr int P = 64 / L;
+  const int lane = threadIdx.x & 63;
+  const int q = lane / L, m = lane % L;
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r0 = gw * P; r0 < n; r0 += nw * P) {
+    const int64_t row = r0 + q;
+    double sq = 0.0;
+    if (q < P && row < n) {
+      const float4 v = *reinterpret_cast<const float4*>(X + row * (4 * L) + 4 * m);
+      sq = (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
     }
-    xnorm[row] = (float)(sqrt(s) * (1.0 + 1e-6)) * 1.0000001f;
+#pragma unroll
+    for (int o = 1; o < L; o <<= 1) sq += __shfl_xor(sq, o);
+    if (q < P && m == 0 && row < n) xnorm[row] = (float)(sqrt(sq) * (1.0 + 1e-6)) * 1.0000001f;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_row_norm_any(const float* __restrict__ X, int64_t n, int dp,
+                                                      float* __restrict__ xnorm) {
+  // one wave per row (lanes over features): dp = 48, 96, 192
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t row = gw; row < n; row += nw) {
+    double sq = 0.0;
+    for (int f = lane; f < dp; f += 64) {
+      const double v = X[row * dp + f];
+      sq = fma(v, v, sq);
+    }
+    sq = wave_sum(sq);
+    if (lane == 0) xnorm[row] = (float)(sqrt(sq) * (1.0 + 1e-6)) * 1.0000001f;
   }
 }
 
@@ -1282,8 +1307,16 @@ hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float
 hipError_t launch_row_norm(const float* X, const Geometry& g, float* xnorm, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
   int64_t blocks = (g.n + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(k_row_norm, dim3((unsigned)blocks), dim3(256), 0, s, X, g.n, g.dp, xnorm);
+  if (blocks > 16384) blocks = 16384;
+  const dim3 grid((unsigned)blocks), blk(256);
+  switch (g.dp / 4) {  // dp in {16, 32, 48, 64, 96, 128, 192, 256}; L must divide 64 -> 48/96/192 use 16 lanes x more
+    case 4: hipLaunchKernelGGL(k_row_norm<4>, grid, blk, 0, s, X, g.n, xnorm); break;
+    case 8: hipLaunchKernelGGL(k_row_norm<8>, grid, blk, 0, s, X, g.n, xnorm); break;
+    case 16: hipLaunchKernelGGL(k_row_norm<16>, grid, blk, 0, s, X, g.n, xnorm); break;
+    case 32: hipLaunchKernelGGL(k_row_norm<32>, grid, blk, 0, s, X, g.n, xnorm); break;
+    case 64: hipLaunchKernelGGL(k_row_norm<64>, grid, blk, 0, s, X, g.n, xnorm); break;
+    default: hipLaunchKernelGGL(k_row_norm_any, grid, blk, 0, s, X, g.n, g.dp, xnorm); break;
+  }
   return hipGetLastError();
 }
 
