@@ -86,6 +86,34 @@ __device__ inline float wave_sum_f(float v) {
   return v;
 }
 
+
+// Screening bound B0 (scaled units, see DESIGN.md "Exactness") for a point of
+// scaled norm xn_s, centroids of scaled max norm cm_s, and the scaled
+// per-feature maxima product pm_s = (cabs s)(xabs s):
+//   fp16x3 split residuals + fp64->fp32 rounding of c + ||c||^2 rounding:
+//       (6.5 2^-22 + 0.5 u) xn cm + u cm^2
+//   accumulation, per MFMA (3 dp/16 of them in a block chain): one final
+//       rounding u |D| <= u (cm^2 + 2 xn cm) plus the in-group alignment
+//       truncation of the v_mfma_f32_32x32x16_f16 product sum, <= 14 u times
+//       the largest product <= 2 pm (characterised in
+//       scripts/probes/mfma_align.hip: terms > 25 bits below their 8-product
+//       group's maximum are dropped; worst observed U|D| + 3.7 u max|term|)
+//   fp16 underflow: u sqrt(dp) (xn + 2 cm)
+// times a 1.5 safety factor.
+// B0 = screen_slope * xn_s + screen_icpt (affine in xn_s)
+__host__ __device__ inline float screen_slope(float cm_s, int dp) {
+  const float nm = 3.0f * (float)dp / 16.0f;  // MFMAs per block chain
+  return 1.5f * ((6.5f * 2.384185791015625e-07f + 0.5f * U24) * cm_s + nm * 2.0f * U24 * cm_s + U24 * sqrtf((float)dp));
+}
+__host__ __device__ inline float screen_icpt(float cm_s, float pm_s, int dp) {
+  const float nm = 3.0f * (float)dp / 16.0f;
+  return 1.5f * (U24 * cm_s * cm_s + nm * (U24 * cm_s * cm_s + 28.0f * U24 * pm_s) +
+                 2.0f * U24 * sqrtf((float)dp) * cm_s);
+}
+__host__ __device__ inline float screen_b0(float xn_s, float cm_s, float pm_s, int dp) {
+  return fmaf(screen_slope(cm_s, dp), xn_s, screen_icpt(cm_s, pm_s, dp));
+}
+
 // ---------------------------------------------------------------------------
 // Centroid preparation: float64 centroids -> fp32 copy (direct screening),
 // bf16 hi/lo split of -2c (MFMA screening), fp32 ||c||^2, max ||c||.
@@ -391,6 +419,7 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
   const uint32_t maskq = (1u << (b - 2)) - 1u;
   const float s = mfma_scale(*A.xabs, *A.cabs);
   const float cm = *A.cmax * s;
+  const float pm = (*A.cabs * s) * (*A.xabs * s) * 1.0001f;
   const float rho = __builtin_ldexpf(1.0f, b - 2 - 23) * 1.01f;  // key truncation (relative)
   const int nchunks = (kp + KC - 1) / KC;
   const int64_t ntiles = (n + 31) / 32;
@@ -577,8 +606,7 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
     // accumulation, ||c||^2 rounding, fp16 underflow (B0); plus the key
     // truncation rho*|K|.  x1.5 safety.
     const float xn = sqrtf(xx) * 1.0001f;
-    const float B0 = 1.5f * ((6.5f * 2.384185791015625e-07f + 0.5f * U24 + (float)(6 * DP + 8) * U24) * xn * cm +
-                             (float)(3 * DP + 5) * U24 * cm * cm + U24 * sqrtf((float)DP) * (xn + 2.0f * cm));
+    const float B0 = screen_b0(xn, cm, pm, DP);
     const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k3));
     const float thr2 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k2));
     // negated tests: NaN (non-finite data) falls through to the full float64
@@ -1145,11 +1173,12 @@ __global__ __launch_bounds__(256) void k_frag_images(const _Float16* __restrict_
 // screening-bound constants: B0 = alpha * ||x|| + beta (see k_assign_mfma)
 __global__ void k_bound_consts(const float* __restrict__ cmax, const float* __restrict__ xabs,
                                const float* __restrict__ cabs, int dp, float* __restrict__ bnd) {
+  // screen_b0 is affine in xn_s = s ||x||: B0 = bnd[0] ||x|| + bnd[1]
   const float s = mfma_scale(*xabs, *cabs);
   const float cm = *cmax * s;
-  const float sq = sqrtf((float)dp);
-  bnd[0] = 1.5f * s * ((6.5f * 2.384185791015625e-07f + 0.5f * U24 + (float)(6 * dp + 8) * U24) * cm + U24 * sq);
-  bnd[1] = 1.5f * ((float)(3 * dp + 5) * U24 * cm * cm + 2.0f * U24 * sq * cm);
+  const float pm = (*cabs * s) * (*xabs * s) * 1.0001f;
+  bnd[0] = screen_slope(cm, dp) * s * 1.0001f;  // per unscaled ||x||
+  bnd[1] = screen_icpt(cm, pm, dp) * 1.0001f;
 }
 
 // upper bound of ||x|| per row (float64 sum, rounded up): L = dp/4 lanes per
