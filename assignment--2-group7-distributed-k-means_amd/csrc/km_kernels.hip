@@ -923,9 +923,9 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       st_acc[0] += tnow - st_last;
       st_last = tnow;
     }
-    float a1[4], a2[4], a3[4];
+    float a1[4], a2[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) a1[c] = a2[c] = a3[c] = FLT_MAX;
+    for (int c = 0; c < 4; ++c) a1[c] = a2[c] = FLT_MAX;
     // the images stay in AGPRs (MFMA A operands read them there); scores
     // land in VGPRs (built with -amdgpu-mfma-vgpr-form)
 #pragma unroll
@@ -959,7 +959,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       return acc;
     };
     // register reg holds centroid j = 32 blk + 4h + (reg & 3) + 8 (reg >> 2);
-    // chain reg & 3 keeps the top three keys (score | j >> 2)
+    // chain reg & 3 keeps the top two keys (score | j >> 2)
     auto keys_block = [&](const f32x16& acc, int blk) {
       if constexpr (ABL == 1 || ABL == 5 || ABL == 6) {
         a1[blk & 3] = fminf(a1[blk & 3], acc[0] + acc[15]);
@@ -970,7 +970,10 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         const float key = __uint_as_float((__float_as_uint(acc[reg]) & ~maskq) | (jq | (uint32_t)(2 * (reg >> 2))));
-        top3_insert(a1[reg & 3], a2[reg & 3], a3[reg & 3], key);
+        const int c = reg & 3;
+        const float n1 = __builtin_amdgcn_fmed3f(a1[c], key, -FLT_MAX);
+        a2[c] = __builtin_amdgcn_fmed3f(a1[c], a2[c], key);
+        a1[c] = n1;
       }
     };
     // software pipeline: block blk's MFMAs overlap block blk-1's key
@@ -1027,15 +1030,18 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       return;
     }
     // top-3 values and best two full indices: chains merged pairwise, then
-    // the two lane halves (disjoint centroid rows of the same point)
+    // the two lane halves.  A chain keeps its best two; keys it dropped are
+    // only known to be >= its second, which therefore stands in for its
+    // third (k3 bounds every candidate other than p1, p2 unless p1 and p2
+    // share a chain: checked below).
     auto pidx = [&](float key, int c) { return ((__float_as_uint(key) & maskq) << 2) | (uint32_t)c; };
-    float k1 = a1[0], k2 = a2[0], k3 = a3[0];
+    float k1 = a1[0], k2 = a2[0], k3 = a2[0];
     uint32_t p1 = pidx(a1[0], 0), p2 = pidx(a2[0], 0);
     {
-      float m1 = a1[2], m2 = a2[2], m3 = a3[2];
+      float m1 = a1[2], m2 = a2[2], m3 = a2[2];
       uint32_t q1 = pidx(a1[2], 2), q2 = pidx(a2[2], 2);
-      merge3(k1, k2, k3, p1, p2, a1[1], a2[1], a3[1], pidx(a1[1], 1), pidx(a2[1], 1));
-      merge3(m1, m2, m3, q1, q2, a1[3], a2[3], a3[3], pidx(a1[3], 3), pidx(a2[3], 3));
+      merge3(k1, k2, k3, p1, p2, a1[1], a2[1], a2[1], pidx(a1[1], 1), pidx(a2[1], 1));
+      merge3(m1, m2, m3, q1, q2, a1[3], a2[3], a2[3], pidx(a1[3], 3), pidx(a2[3], 3));
       merge3(k1, k2, k3, p1, p2, m1, m2, m3, q1, q2);
     }
     {
@@ -1052,16 +1058,14 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       p2 = P2;
       merge3(k1, k2, k3, p1, p2, __uint_as_float(Q1), __uint_as_float(Q2), __uint_as_float(Q3), R1, R2);
     }
-    // every candidate other than p1, p2 is >= k3 (a chain drops only keys
-    // above its kept third)
+    // p1, p2 in one chain (same j & 3 and lane half): that chain's dropped
+    // keys are only known to be >= k2, so no re-rank certificate (full scan)
+    const bool same_chain = ((p1 ^ p2) & 7u) == 0u;
     const float B0 = fmaf(alpha, xn, beta);
     const float thr2 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k2));
     const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k3));
     uint32_t kind = 0;
-    if (!(k3 - k1 > thr3))
-      kind = 2;
-    else if (!(k2 - k1 > thr2))
-      kind = 1;
+    if (!(k2 - k1 > thr2)) kind = (same_chain || !(k3 - k1 > thr3)) ? 2u : 1u;
     if constexpr (ABL == 7) {
       __builtin_amdgcn_sched_barrier(0);
       const unsigned long long tnow = __builtin_amdgcn_s_memtime();
