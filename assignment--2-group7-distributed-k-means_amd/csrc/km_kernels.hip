@@ -171,7 +171,9 @@ hipError_t launch_prep_centroids(const double* C64, const Geometry& g, float* C3
 static constexpr int SMALL_MAX_K = 32;
 static constexpr int SMALL_LDS = 60 * 1024;
 
-template <int DP>
+// KU > 0: k <= KU, loops over centroids unrolled and the fp32 centroids held
+// in registers (no LDS reads queued behind the statistics atomics)
+template <int DP, int KU = 0>
 __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k,
                                                       const float* __restrict__ C32,
                                                       const double* __restrict__ C64,
@@ -194,29 +196,60 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
   const float beta = 2.0f * 2.5f * U24 * cm;
   const float g0 = 2.0f * 8.0f * U24 * U24 * cm * cm;
   const int rep = threadIdx.x & (R - 1);
+  float cr[KU > 0 ? KU : 1][DP];
+  if constexpr (KU > 0) {
+#pragma unroll
+    for (int j = 0; j < KU; ++j)
+#pragma unroll
+      for (int f = 0; f < DP; ++f) cr[j][f] = j < k ? sC[j * DP + f] : 0.0f;
+  }
 
-  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < n;
-       row += (int64_t)gridDim.x * blockDim.x) {
-    const float* xr = X + row * DP;
+  // rows strided over the grid; the next row is prefetched into registers
+  // while this one is processed (the loop is otherwise latency-bound)
+  const int64_t rstride = (int64_t)gridDim.x * blockDim.x;
+  int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float4 nx[DP / 4];
+  if (row < n) {
+#pragma unroll
+    for (int f = 0; f < DP; f += 4) nx[f / 4] = *reinterpret_cast<const float4*>(X + row * DP + f);
+  }
+  for (; row < n; row += rstride) {
     float x[DP];
 #pragma unroll
     for (int f = 0; f < DP; f += 4) {
-      const float4 v = *reinterpret_cast<const float4*>(xr + f);
+      const float4 v = nx[f / 4];
       x[f] = v.x;
       x[f + 1] = v.y;
       x[f + 2] = v.z;
       x[f + 3] = v.w;
     }
-    float k1 = FLT_MAX, k2 = FLT_MAX, k3 = FLT_MAX;
-    for (int j = 0; j < k; ++j) {
-      const float* c = sC + j * DP;
-      float acc = 0.0f;
+    if (row + rstride < n) {
 #pragma unroll
-      for (int f = 0; f < DP; ++f) {
-        const float t = x[f] - c[f];
-        acc = fmaf(t, t, acc);
+      for (int f = 0; f < DP; f += 4) nx[f / 4] = *reinterpret_cast<const float4*>(X + (row + rstride) * DP + f);
+    }
+    float k1 = FLT_MAX, k2 = FLT_MAX, k3 = FLT_MAX;
+    if constexpr (KU > 0) {
+#pragma unroll
+      for (int j = 0; j < KU; ++j) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int f = 0; f < DP; ++f) {
+          const float t = x[f] - cr[j][f];
+          acc = fmaf(t, t, acc);
+        }
+        if (j < k) top3_insert(k1, k2, k3, key_of(acc, (uint32_t)j, mask));
       }
-      top3_insert(k1, k2, k3, key_of(acc, (uint32_t)j, mask));
+    } else {
+      for (int j = 0; j < k; ++j) {
+        const float* c = sC + j * DP;
+        float acc = 0.0f;
+#pragma unroll
+        for (int f = 0; f < DP; ++f) {
+          const float t = x[f] - c[f];
+          acc = fmaf(t, t, acc);
+        }
+        top3_insert(k1, k2, k3, key_of(acc, (uint32_t)j, mask));
+      }
     }
     int lab = (int)(__float_as_uint(k1) & mask);
     const int i2 = (int)(__float_as_uint(k2) & mask);
@@ -268,9 +301,16 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
   }
 }
 
+// tuning knobs (defaults measured on MI355X; env overrides for sweeps)
+static int small_env(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
 static int small_replicas(const Geometry& g) {
   const size_t cbytes = ((size_t)g.k * g.dp * 4 + 15) / 16 * 16;
-  int R = 32;
+  static const int rmax = small_env("KM_SMALL_R", 32);
+  int R = rmax;
   while (R > 1 && cbytes + (size_t)g.k * (g.d + 1) * 8 * R > SMALL_LDS) R >>= 1;
   return R;
 }
@@ -288,7 +328,8 @@ hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C
   const int R = small_replicas(g);
   const size_t lds = ((size_t)g.k * g.dp * 4 + 15) / 16 * 16 + (fuse ? (size_t)g.k * (g.d + 1) * 8 * R : 0);
   int64_t blocks = (g.n + 255) / 256;
-  const int64_t cap = (int64_t)n_cu * 4;
+  static const int bpc = small_env("KM_SMALL_BPC", 4);
+  const int64_t cap = (int64_t)n_cu * bpc;
   if (blocks > cap) blocks = cap;
   switch (g.dp) {
     case 16:
