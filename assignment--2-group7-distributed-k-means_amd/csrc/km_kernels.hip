@@ -8,6 +8,7 @@
 // whether the screened best is provably the float64 best, whether the top-2
 // must be re-ranked in float64, or whether a full float64 scan is needed.
 // Neither path ever returns a label the float64 argmin would not.
+#include "km_exact.h"
 #include "km_internal.h"
 
 #include <float.h>
@@ -39,39 +40,6 @@ __device__ __forceinline__ void top3_insert(float& k1, float& k2, float& k3, flo
 
 __device__ __forceinline__ float key_of(float score, uint32_t idx, uint32_t mask) {
   return __uint_as_float((__float_as_uint(score) & ~mask) | idx);
-}
-
-// ||x - c||^2 in float64 (x fp32 row with stride, c float64 row)
-__device__ inline double d2_exact(const float* __restrict__ x, const double* __restrict__ c, int d) {
-  double s = 0.0;
-  for (int f = 0; f < d; ++f) {
-    const double t = (double)x[f] - c[f];
-    s = fma(t, t, s);
-  }
-  return s;
-}
-
-// Full float64 scan, first minimum wins (np.argmin, kmeans_spark.py:156).
-__device__ inline int exact_argmin(const float* __restrict__ x, const double* __restrict__ C64, int k, int d) {
-  double best = d2_exact(x, C64, d);
-  int lab = 0;
-  for (int j = 1; j < k; ++j) {
-    const double v = d2_exact(x, C64 + (size_t)j * d, d);
-    if (v < best) {
-      best = v;
-      lab = j;
-    }
-  }
-  return lab;
-}
-
-__device__ inline int exact_pick2(const float* __restrict__ x, const double* __restrict__ C64, int d, int a,
-                                  int b) {
-  const double va = d2_exact(x, C64 + (size_t)a * d, d);
-  const double vb = d2_exact(x, C64 + (size_t)b * d, d);
-  if (va < vb) return a;
-  if (vb < va) return b;
-  return a < b ? a : b;
 }
 
 __device__ inline double wave_sum(double v) {
@@ -259,23 +227,15 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
     const bool need_full = (k >= 3) && !((k3 > 64.0f * U24 * U24 * cm * cm) && (k3 - B3 > k1 + B1));
     const bool need_two = (k >= 2) && !(k2 - B2 > k1 + B1);
     if (need_full || need_two) {
-      // exact float64 distances with the point held in registers
+      // the reference's float64 norms with the point held in registers
       double best = 0.0;
       int bl = -1;
       const int jn = need_full ? k : 2;
       for (int jj = 0; jj < jn; ++jj) {
         const int j = need_full ? jj : (jj == 0 ? (lab < i2 ? lab : i2) : (lab < i2 ? i2 : lab));
-        const double* c = C64 + (size_t)j * d;
-        double s = 0.0;
-#pragma unroll
-        for (int f = 0; f < DP; ++f) {
-          if (f < d) {
-            const double t = (double)x[f] - c[f];
-            s = fma(t, t, s);
-          }
-        }
-        if (bl < 0 || s < best) {
-          best = s;
+        const double v = np_norm_reg<DP>(x, C64 + (size_t)j * d, d);
+        if (np_better(v, best, bl >= 0)) {
+          best = v;
           bl = j;
         }
       }
@@ -1465,7 +1425,9 @@ __device__ __forceinline__ uint32_t find_segment(const uint32_t* __restrict__ pr
 // sums (the fused kernel leaves every queued point to the resolvers): into an
 // LDS table [f][j] flushed at the end when it fits (tab_kp > 0), else with
 // global float64 atomics.  The entries of all segments are spread over all
-// waves of the grid (16 lanes per entry, 4 entries per wave-iteration).
+// lanes of the grid, one entry per lane: each lane evaluates the two
+// candidates' norms in NumPy's summation order (np_norm), which is sequential
+// per accumulator, so a lane-parallel split would change the rounding.
 __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, int dp, int d, int k,
                                                   const double* __restrict__ C64, const QEntry* __restrict__ queue,
                                                   const uint32_t* __restrict__ qcount, QLayout ql,
@@ -1478,89 +1440,38 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
     for (int i = threadIdx.x; i < d * tab_kp; i += blockDim.x) tab[i] = 0.0;
   block_prefix(qcount, 0, ql.nwaves, pre);
   const uint32_t total = pre[ql.nwaves];
-  const int lane = threadIdx.x & 63;
-  const int sub = lane >> 4;   // entry slot in the wave
-  const int m = lane & 15;     // features 4m..4m+3 (+64t)
-  const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
-  for (uint32_t g0 = gw * 4; g0 < total; g0 += nw * 4) {
-    {
-      const uint32_t g = g0 + (uint32_t)sub;
-      const bool have = g < total;
-      QEntry q{0, 0, 0, 0};
-      if (have) {
-        const uint32_t sg = find_segment(pre, ql.nwaves, g);
-        q = queue[(size_t)sg * ql.seg + (g - pre[sg])];
-      }
-      const bool ok = have && q.i1 < (uint32_t)k && q.i2 < (uint32_t)k;
-      double s1 = 0.0, s2 = 0.0;
-      if (ok) {
-        const float* x = X + (size_t)q.row * dp;
-        const double* ca = C64 + (size_t)q.i1 * d;
-        const double* cb = C64 + (size_t)q.i2 * d;
-        for (int f0 = 4 * m; f0 < d; f0 += 64) {
-          const float4 xv = *reinterpret_cast<const float4*>(x + f0);
-          const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            if (f0 + c < d) {
-              const double xf = (double)xs[c];
-              const double ta = xf - ca[f0 + c];
-              const double tb = xf - cb[f0 + c];
-              s1 = fma(ta, ta, s1);
-              s2 = fma(tb, tb, s2);
-            }
-          }
+  const uint32_t nt = gridDim.x * blockDim.x;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < total; g += nt) {
+    const uint32_t sg = find_segment(pre, ql.nwaves, g);
+    const QEntry q = queue[(size_t)sg * ql.seg + (g - pre[sg])];
+    const float* __restrict__ x = X + (size_t)q.row * dp;
+    int lab = 0;
+    if (q.i1 < (uint32_t)k && q.i2 < (uint32_t)k) {
+      const int a = (int)min(q.i1, q.i2), bb = (int)max(q.i1, q.i2);
+      const double* __restrict__ ca = C64 + (size_t)a * d;
+      const double* __restrict__ cb = C64 + (size_t)bb * d;
+      const double va = np_norm([&](int f) { return np_sq(ca[f], x[f]); }, d);
+      const double vb = np_norm([&](int f) { return np_sq(cb[f], x[f]); }, d);
+      lab = np_pick_second(va, vb) ? bb : a;
+    } else {
+      // corrupt candidate (cannot happen for finite data): full scan
+      double best = 0.0;
+      for (int j = 0; j < k; ++j) {
+        const double* __restrict__ c = C64 + (size_t)j * d;
+        const double v = np_norm([&](int f) { return np_sq(c[f], x[f]); }, d);
+        if (np_better(v, best, j > 0)) {
+          best = v;
+          lab = j;
         }
       }
-#pragma unroll
-      for (int o = 8; o >= 1; o >>= 1) {
-        s1 += __shfl_xor(s1, o);
-        s2 += __shfl_xor(s2, o);
-      }
-      int lab = -1;
-      if (ok) {
-        const bool first_a = q.i1 < q.i2;
-        const int a = (int)(first_a ? q.i1 : q.i2), bb = (int)(first_a ? q.i2 : q.i1);
-        const double sa = first_a ? s1 : s2, sb = first_a ? s2 : s1;
-        lab = (sb < sa) ? bb : a;  // ties and NaN keep the lower index
-        if (m == 0) labels[q.row] = lab;
-      }
-      if (ok && stats) {
-        const float* x = X + (size_t)q.row * dp;
-        for (int f0 = 4 * m; f0 < d; f0 += 64) {
-          const float4 xv = *reinterpret_cast<const float4*>(x + f0);
-          const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-            if (f0 + c < d) {
-              if (tab_kp)
-                atomicAdd(tab + (size_t)(f0 + c) * tab_kp + lab, (double)xs[c]);
-              else
-                atomicAdd(stats + (size_t)lab * (d + 1) + f0 + c, (double)xs[c]);
-            }
-        }
-      }
-      if (have && !ok && m == 0) {
-        // corrupt candidate (cannot happen for finite data): exact scan
-        const float* x = X + (size_t)q.row * dp;
-        double best = 0.0;
-        int bl = 0;
-        for (int j = 0; j < k; ++j) {
-          double t2 = 0.0;
-          for (int f = 0; f < d; ++f) {
-            const double t = (double)x[f] - C64[(size_t)j * d + f];
-            t2 = fma(t, t, t2);
-          }
-          if (j == 0 || t2 < best) {
-            best = t2;
-            bl = j;
-          }
-        }
-        labels[q.row] = bl;
-        if (stats) {
-          for (int f = 0; f < d; ++f) atomicAdd(stats + (size_t)bl * (d + 1) + f, (double)x[f]);
-        }
+    }
+    labels[q.row] = lab;
+    if (stats) {
+      for (int f = 0; f < d; ++f) {
+        if (tab_kp)
+          atomicAdd(tab + (size_t)f * tab_kp + lab, (double)x[f]);
+        else
+          atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)x[f]);
       }
     }
   }
@@ -1575,6 +1486,8 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
   }
 }
 
+// point rows staged per wave for the full scan (d <= 256 floats)
+static constexpr int FS_XS_BYTES = 16 * 256 * 4;
 
 __global__ __launch_bounds__(1024) void k_fullscan(const float* __restrict__ X, int dp, int d, int k,
                                                    const double* __restrict__ C64T, const QEntry* __restrict__ queue,
@@ -1583,63 +1496,69 @@ __global__ __launch_bounds__(1024) void k_fullscan(const float* __restrict__ X, 
                                                    double* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sCT = reinterpret_cast<double*>(smem);
-  uint32_t* pre = reinterpret_cast<uint32_t*>(smem + (use_lds ? (size_t)k * d * 8 : 0));
+  const size_t ct_bytes = use_lds ? (size_t)k * d * 8 : 0;
+  float* xs_all = reinterpret_cast<float*>(smem + ct_bytes);
+  uint32_t* pre = reinterpret_cast<uint32_t*>(smem + ct_bytes + FS_XS_BYTES);
   if (use_lds)
     for (int i = threadIdx.x; i < k * d; i += blockDim.x) sCT[i] = C64T[i];
   block_prefix(qcount, 1, ql.nwaves, pre);
   const uint32_t total = pre[ql.nwaves];
   const double* CT = use_lds ? sCT : C64T;
   const int lane = threadIdx.x & 63;
+  float* xs = xs_all + (threadIdx.x >> 6) * 256;
   const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
   // one wave per entry, entries of all segments spread over all waves; the
-  // point's row is held one feature per lane and broadcast with v_readlane;
-  // lanes run over centroids (C64T rows are contiguous in j).  Full-scan
-  // entries sit at the back of each segment.
+  // point's row is staged in this wave's LDS slot and read as a broadcast;
+  // lanes run over centroids (C64T rows are contiguous in j), each evaluating
+  // the reference's norm in NumPy's order.  Full-scan entries sit at the back
+  // of each segment.
   for (uint32_t g = gw; g < total; g += nw) {
-    {
-      const uint32_t sg = find_segment(pre, ql.nwaves, g);
-      const uint32_t e = g - pre[sg];
-      const QEntry* qp = queue + (size_t)sg * ql.seg + (ql.seg - 1u - e);
-      const uint32_t row = __builtin_amdgcn_readfirstlane(qp->row);
-      const float* x = X + (size_t)row * dp;
-      double best = 0.0;
-      int bj = 0x7fffffff;
-      for (int j0 = 0; j0 < k; j0 += 64) {
-        const int j = min(j0 + lane, k - 1);
-        double acc = 0.0;
-        for (int f0 = 0; f0 < d; f0 += 64) {
-          const float xl = (f0 + lane < d) ? x[f0 + lane] : 0.0f;
-          const int fe = min(64, d - f0);
-          const double* ct = CT + (size_t)f0 * k + j;
-#pragma unroll 8
-          for (int f = 0; f < 64; ++f) {
-            if (f < fe) {
-              const float xf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xl), f));
-              const double t = (double)xf - ct[(size_t)f * k];
-              acc = fma(t, t, acc);
-            }
-          }
-        }
-        if (j0 + lane < k && !(acc != acc) && (bj == 0x7fffffff || acc < best)) {
-          best = acc;
+    const uint32_t sg = find_segment(pre, ql.nwaves, g);
+    const uint32_t e = g - pre[sg];
+    const QEntry* qp = queue + (size_t)sg * ql.seg + (ql.seg - 1u - e);
+    const uint32_t row = __builtin_amdgcn_readfirstlane(qp->row);
+    const float* x = X + (size_t)row * dp;
+    for (int f = lane; f < d; f += 64) xs[f] = x[f];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    double best = 0.0;
+    int bj = -1;
+    for (int j0 = 0; j0 < k; j0 += 64) {
+      const int j = j0 + lane;
+      if (j < k) {
+        const double* ct = CT + j;
+        const double v = np_norm([&](int f) { return np_sq(ct[(size_t)f * k], xs[f]); }, d);
+        if (np_better(v, best, bj >= 0)) {
+          best = v;
           bj = j;
         }
       }
+    }
+    // np.argmin across lanes: first NaN, else smallest value, lowest index
 #pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) {
-        const double ob = __shfl_xor(best, o);
-        const int oj = __shfl_xor(bj, o);
-        if (oj != 0x7fffffff && (bj == 0x7fffffff || ob < best || (ob == best && oj < bj))) {
-          best = ob;
-          bj = oj;
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double ob = __shfl_xor(best, o);
+      const int oj = __shfl_xor(bj, o);
+      bool take = false;
+      if (oj >= 0) {
+        if (bj < 0) {
+          take = true;
+        } else {
+          const bool on = ob != ob, mn = best != best;
+          take = (on && !mn) || (on == mn && (on ? oj < bj : (ob < best || (ob == best && oj < bj))));
         }
       }
-      const int lab = (bj == 0x7fffffff) ? 0 : bj;  // all-NaN distances: np.argmin -> 0
-      if (lane == 0) labels[row] = lab;
-      if (stats)
-        for (int f = lane; f < d; f += 64) atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)x[f]);
+      if (take) {
+        best = ob;
+        bj = oj;
+      }
     }
+    const int lab = bj < 0 ? 0 : bj;
+    if (lane == 0) labels[row] = lab;
+    if (stats)
+      for (int f = lane; f < d; f += 64) atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)xs[f]);
+    __builtin_amdgcn_wave_barrier();  // xs reused by the next entry
   }
 }
 
@@ -1656,9 +1575,11 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
                      C64, queue, qcount, ql, labels, stats, tab_kp);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (g.d > 256) return hipErrorInvalidValue;
   const size_t bytes = (size_t)g.k * g.d * 8;
-  const int use_lds = bytes + pre_bytes <= LDS_MAX ? 1 : 0;
-  hipLaunchKernelGGL(k_fullscan, dim3(n_cu), dim3(1024), (use_lds ? bytes : 0) + pre_bytes, s, X, g.dp, g.d, g.k,
+  const int use_lds = bytes + FS_XS_BYTES + pre_bytes <= LDS_MAX ? 1 : 0;
+  hipLaunchKernelGGL(k_fullscan, dim3(n_cu), dim3(1024), (use_lds ? bytes : 0) + FS_XS_BYTES + pre_bytes, s, X,
+                     g.dp, g.d, g.k,
                      C64T, queue, qcount, ql, labels, use_lds, stats);
   return hipGetLastError();
 }

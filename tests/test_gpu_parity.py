@@ -130,6 +130,9 @@ def _check_labels(X, C, labels):
     (12345, 17, 40, 10),       # d=17 -> 32 padded, k not a multiple of 32
     (9999, 100, 70, 20),       # d=100 -> 128 padded
     (4000, 200, 33, 33),       # d=200 -> 256 padded
+    (40, 64, 36, 8),           # two 32-point tiles, the second partial (fused kernel tail)
+    (1000, 40, 70, 10),        # d=40 -> 48 padded (fused <3,4>, generic row norms)
+    (5000, 64, 300, 60),       # k=300 -> kp=320: unfused MFMA path + LDS-range statistics
 ])
 def test_one_step_vs_oracle(n, d, k, centers):
     X = _blobs(n, d, centers, seed=n + d + k)
@@ -183,3 +186,25 @@ def test_predict_requires_fit():
     ka = _km()
     with pytest.raises(ValueError, match="Model must be fitted before prediction"):
         ka.KMeans(k=2).predict(np.zeros((5, 2)))
+
+
+@pytest.mark.parametrize("n,d,nb,off", [
+    (20000, 64, 128, 128),   # fused kernel, duplicates on the same chain -> full scans
+    (20000, 64, 127, 127),   # fused kernel, duplicates on other chains -> pair re-rank
+    (20000, 16, 12, 12),     # small path (k <= 32): in-thread re-rank / full scan
+    (8000, 100, 150, 150),   # unfused MFMA path (kp = 320)
+    (6000, 200, 40, 40),     # d = 200: pairwise split 96 + 104
+    (6000, 250, 20, 20),     # d = 250: split 120 + (64 + 66), two levels
+])
+def test_near_ties_one_ulp_apart_vs_oracle(n, d, nb, off):
+    # centroids duplicated and nudged by one float64 ulp: every point is a
+    # near-tie the screen cannot separate; the float64 resolvers must return
+    # np.argmin over np.linalg.norm bit for bit (kmeans_spark.py:153-156)
+    X = _blobs(n, d, 64, 11 + d)
+    rng = np.random.default_rng(5 + d)
+    base = X[rng.choice(len(X), nb, replace=False)]
+    C0 = np.concatenate([base, np.nextafter(base, np.inf)])
+    assert len(C0) == nb + off
+    labels = _one_step(X, C0, iters=1)._runner.engine.labels()
+    lab_ref = orc.assign(X, C0)[0]
+    np.testing.assert_array_equal(labels, lab_ref)

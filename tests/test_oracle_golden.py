@@ -66,3 +66,48 @@ def test_oracle_validation_messages():
         orc.lloyd_fit(X, 2, tolerance=0)
     with pytest.raises(ValueError, match=r"Not enough data points \(4\) to initialize 5 clusters"):
         orc.lloyd_fit(X, 5)
+
+
+def _np_order_norm(c, x):
+    """The summation order the HIP resolvers implement (km_kernels.hip np_norm):
+    rounded (c - x)^2 terms, NumPy pairwise_sum blocks of <= 128 with 8
+    strided accumulators, halves split at n/2 rounded down to a multiple of 8."""
+    t = [(float(cf) - float(xf)) * (float(cf) - float(xf)) for cf, xf in zip(c, x)]
+
+    def block(a):
+        if len(a) < 8:
+            r = 0.0
+            for v in a:
+                r += v
+            return r
+        r = list(a[:8])
+        nm = len(a) - len(a) % 8
+        for i in range(8, nm, 8):
+            for u in range(8):
+                r[u] += a[i + u]
+        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+        for v in a[nm:]:
+            res += v
+        return res
+
+    def pw(a):
+        if len(a) <= 128:
+            return block(a)
+        n2 = len(a) // 2
+        n2 -= n2 % 8
+        return pw(a[:n2]) + pw(a[n2:])
+
+    return np.sqrt(pw(t))
+
+
+@pytest.mark.parametrize("d", [1, 2, 7, 8, 9, 15, 16, 17, 64, 100, 127, 128, 129, 136, 200, 250, 255, 256])
+def test_resolver_summation_order_is_linalg_norm(d):
+    # near-tie centroids (one float64 ulp apart) make any other order show
+    rng = np.random.default_rng(d)
+    X = (rng.standard_normal((40, d)) * 5).astype(np.float32).astype(np.float64)
+    base = rng.standard_normal((6, d)) * 5
+    C = np.concatenate([base, np.nextafter(base, np.inf), np.nextafter(base, -np.inf)])
+    for x in X:
+        ref = np.linalg.norm(C - x, axis=1)
+        got = np.array([_np_order_norm(c, x) for c in C])
+        np.testing.assert_array_equal(got, ref)
