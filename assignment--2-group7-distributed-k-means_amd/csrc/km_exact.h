@@ -109,6 +109,69 @@ __device__ inline double np_norm_reg(const float (&x)[DP], const double* __restr
   return sqrt(res);
 }
 
+// Cooperative form: 8 consecutive lanes (u = lane & 7) evaluate one norm,
+// lane u holding NumPy's accumulator r[u]; the xor-butterfly over 1, 2, 4
+// forms exactly ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) (IEEE addition is
+// commutative), after which every lane holds the block sum and adds the
+// remainder terms itself.  SQ2 evaluates two norms (a, b) at once.
+template <class SQ2>
+__device__ inline void np_pw_block8(const SQ2& sq, int lo, int n, int u, double& sa, double& sb) {
+#pragma clang fp contract(off)
+  double ra = 0.0, rb = 0.0;
+  if (n < 8) {
+    for (int i = 0; i < n; ++i) {
+      double ta, tb;
+      sq(lo + i, ta, tb);
+      ra = np_add(ra, ta);
+      rb = np_add(rb, tb);
+    }
+    sa = ra;
+    sb = rb;
+    return;
+  }
+  sq(lo + u, ra, rb);
+  const int nm = n - (n & 7);
+  for (int i = 8; i < nm; i += 8) {
+    double ta, tb;
+    sq(lo + i + u, ta, tb);
+    ra = np_add(ra, ta);
+    rb = np_add(rb, tb);
+  }
+#pragma unroll
+  for (int o = 1; o <= 4; o <<= 1) {
+    ra = np_add(ra, __shfl_xor(ra, o));
+    rb = np_add(rb, __shfl_xor(rb, o));
+  }
+  for (int i = nm; i < n; ++i) {
+    double ta, tb;
+    sq(lo + i, ta, tb);
+    ra = np_add(ra, ta);
+    rb = np_add(rb, tb);
+  }
+  sa = ra;
+  sb = rb;
+}
+
+template <int DEPTH, class SQ2>
+__device__ inline void np_pw8(const SQ2& sq, int lo, int n, int u, double& sa, double& sb) {
+#pragma clang fp contract(off)
+  if constexpr (DEPTH == 0) {
+    np_pw_block8(sq, lo, n, u, sa, sb);
+  } else {
+    if (n <= 128) {
+      np_pw_block8(sq, lo, n, u, sa, sb);
+      return;
+    }
+    int n2 = n >> 1;
+    n2 -= n2 & 7;
+    double a1, b1, a2, b2;
+    np_pw8<DEPTH - 1>(sq, lo, n2, u, a1, b1);
+    np_pw8<DEPTH - 1>(sq, lo + n2, n - n2, u, a2, b2);
+    sa = np_add(a1, a2);
+    sb = np_add(b1, b2);
+  }
+}
+
 // np.argmin update in ascending index order: the first NaN wins, else the
 // first strict minimum
 __device__ __forceinline__ bool np_better(double v, double best, bool have) {

@@ -1425,9 +1425,8 @@ __device__ __forceinline__ uint32_t find_segment(const uint32_t* __restrict__ pr
 // sums (the fused kernel leaves every queued point to the resolvers): into an
 // LDS table [f][j] flushed at the end when it fits (tab_kp > 0), else with
 // global float64 atomics.  The entries of all segments are spread over all
-// lanes of the grid, one entry per lane: each lane evaluates the two
-// candidates' norms in NumPy's summation order (np_norm), which is sequential
-// per accumulator, so a lane-parallel split would change the rounding.
+// waves of the grid, 8 lanes per entry (np_pw8: lane u owns NumPy's
+// accumulator u, so the rounding is the reference's), 8 entries per wave.
 __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, int dp, int d, int k,
                                                   const double* __restrict__ C64, const QEntry* __restrict__ queue,
                                                   const uint32_t* __restrict__ qcount, QLayout ql,
@@ -1440,20 +1439,32 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
     for (int i = threadIdx.x; i < d * tab_kp; i += blockDim.x) tab[i] = 0.0;
   block_prefix(qcount, 0, ql.nwaves, pre);
   const uint32_t total = pre[ql.nwaves];
-  const uint32_t nt = gridDim.x * blockDim.x;
-  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < total; g += nt) {
-    const uint32_t sg = find_segment(pre, ql.nwaves, g);
-    const QEntry q = queue[(size_t)sg * ql.seg + (g - pre[sg])];
+  const int u = threadIdx.x & 7;
+  const uint32_t ng = (gridDim.x * blockDim.x) >> 3;
+  // the loop trip count is uniform over each 8-lane group (shuffles inside)
+  for (uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 3; g < total + ((ng - total % ng) % ng);
+       g += ng) {
+    const bool have = g < total;
+    QEntry q{0, 0, 0, 0};
+    if (have) {
+      const uint32_t sg = find_segment(pre, ql.nwaves, g);
+      q = queue[(size_t)sg * ql.seg + (g - pre[sg])];
+    }
+    const bool ok = have && q.i1 < (uint32_t)k && q.i2 < (uint32_t)k;
+    const int a = ok ? (int)min(q.i1, q.i2) : 0, bb = ok ? (int)max(q.i1, q.i2) : 0;
     const float* __restrict__ x = X + (size_t)q.row * dp;
-    int lab = 0;
-    if (q.i1 < (uint32_t)k && q.i2 < (uint32_t)k) {
-      const int a = (int)min(q.i1, q.i2), bb = (int)max(q.i1, q.i2);
-      const double* __restrict__ ca = C64 + (size_t)a * d;
-      const double* __restrict__ cb = C64 + (size_t)bb * d;
-      const double va = np_norm([&](int f) { return np_sq(ca[f], x[f]); }, d);
-      const double vb = np_norm([&](int f) { return np_sq(cb[f], x[f]); }, d);
-      lab = np_pick_second(va, vb) ? bb : a;
-    } else {
+    const double* __restrict__ ca = C64 + (size_t)a * d;
+    const double* __restrict__ cb = C64 + (size_t)bb * d;
+    double sa, sb;
+    np_pw8<2>([&](int f, double& ta, double& tb) {
+                const float xf = x[f];
+                ta = np_sq(ca[f], xf);
+                tb = np_sq(cb[f], xf);
+              },
+              0, d, u, sa, sb);
+    if (!have) continue;
+    int lab = np_pick_second(sqrt(sa), sqrt(sb)) ? bb : a;
+    if (!ok && u == 0) {
       // corrupt candidate (cannot happen for finite data): full scan
       double best = 0.0;
       for (int j = 0; j < k; ++j) {
@@ -1465,9 +1476,10 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
         }
       }
     }
-    labels[q.row] = lab;
+    if (!ok) lab = __shfl(lab, (int)(threadIdx.x & 63) & ~7);
+    if (u == 0) labels[q.row] = lab;
     if (stats) {
-      for (int f = 0; f < d; ++f) {
+      for (int f = u; f < d; f += 8) {
         if (tab_kp)
           atomicAdd(tab + (size_t)f * tab_kp + lab, (double)x[f]);
         else
