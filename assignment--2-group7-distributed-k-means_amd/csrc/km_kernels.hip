@@ -1367,18 +1367,19 @@ hipError_t launch_count(const int32_t* labels, const Geometry& g, double* stats,
 // first-minimum tie-break, kmeans_spark.py:153-156).
 //   k_rerank2:   {i1, i2} re-ranked, 16 lanes per entry (4 entries per wave,
 //                float4 / double2 loads, all issued before use).
-//   k_fullscan:  full scan, one wave per entry, lanes over centroids, the
-//                transposed float64 centroids C64T[d][k] staged in LDS when
-//                they fit (read from L2 otherwise).
+//   k_fullscan:  full scan, G entries per wave, lanes over centroids, the
+//                transposed float64 centroids C64T[d][k] streamed through
+//                LDS in column chunks shared by the workgroup's entries.
 // Walks the per-wave queue segments written by k_assign_mfma.
 // ---------------------------------------------------------------------------
 // Exclusive prefix over the per-segment queue counts (word `which` of each
-// count pair) into LDS pre[0..nseg]; blockDim.x == 1024.
+// count pair) into LDS pre[0..nseg]; blockDim.x a multiple of 64, <= 1024.
 __device__ void block_prefix(const uint32_t* __restrict__ qcount, int which, uint32_t nseg,
                              uint32_t* __restrict__ pre) {
   __shared__ uint32_t wsum[16];
   const uint32_t t = threadIdx.x;
-  const uint32_t chunk = (nseg + 1023u) / 1024u;
+  const uint32_t nt = blockDim.x;
+  const uint32_t chunk = (nseg + nt - 1u) / nt;
   const uint32_t b0 = t * chunk;
   uint32_t v = 0;
   for (uint32_t i = 0; i < chunk; ++i)
@@ -1400,9 +1401,9 @@ __device__ void block_prefix(const uint32_t* __restrict__ qcount, int which, uin
       pre[b0 + i] = run;
       run += qcount[2 * (b0 + i) + which];
     }
-  if (t == 1023) {
+  if (t == nt - 1) {
     uint32_t tot = 0;
-    for (int i = 0; i < 16; ++i) tot += wsum[i];
+    for (uint32_t i = 0; i < nt / 64; ++i) tot += wsum[i];
     pre[nseg] = tot;
   }
   __syncthreads();
@@ -1498,79 +1499,105 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
   }
 }
 
-// point rows staged per wave for the full scan (d <= 256 floats)
-static constexpr int FS_XS_BYTES = 16 * 256 * 4;
-
-__global__ __launch_bounds__(1024) void k_fullscan(const float* __restrict__ X, int dp, int d, int k,
+// Full exact scans.  A workgroup (8 waves) takes batches of 8 G queued
+// points, G per wave; the transposed centroids stream through LDS in chunks
+// of ch columns ([d][ch] doubles), each chunk serving all 8 G points, so
+// C64T is read once per batch instead of once per point (at k = 4096,
+// d = 128 it is 4 MiB).  Lane j of a wave evaluates centroid c0 + j for
+// each of its G points in NumPy's order (np_norm), from the chunk (one
+// conflict-free double per lane) and the point's row staged in LDS
+// (broadcast reads).  Full-scan entries sit at the back of each segment.
+template <int G>
+__global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, int dp, int d, int k,
                                                    const double* __restrict__ C64T, const QEntry* __restrict__ queue,
                                                    const uint32_t* __restrict__ qcount, QLayout ql,
-                                                   int32_t* __restrict__ labels, int use_lds,
+                                                   int32_t* __restrict__ labels, int ch,
                                                    double* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* sCT = reinterpret_cast<double*>(smem);
-  const size_t ct_bytes = use_lds ? (size_t)k * d * 8 : 0;
-  float* xs_all = reinterpret_cast<float*>(smem + ct_bytes);
-  uint32_t* pre = reinterpret_cast<uint32_t*>(smem + ct_bytes + FS_XS_BYTES);
-  if (use_lds)
-    for (int i = threadIdx.x; i < k * d; i += blockDim.x) sCT[i] = C64T[i];
+  double* sCT = reinterpret_cast<double*>(smem);                                    // [d][ch]
+  float* xs_all = reinterpret_cast<float*>(smem + (size_t)d * ch * 8);              // [8][G][d]
+  uint32_t* pre = reinterpret_cast<uint32_t*>(smem + (size_t)d * ch * 8 + (size_t)8 * G * d * 4);
   block_prefix(qcount, 1, ql.nwaves, pre);
   const uint32_t total = pre[ql.nwaves];
-  const double* CT = use_lds ? sCT : C64T;
   const int lane = threadIdx.x & 63;
-  float* xs = xs_all + (threadIdx.x >> 6) * 256;
-  const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
-  // one wave per entry, entries of all segments spread over all waves; the
-  // point's row is staged in this wave's LDS slot and read as a broadcast;
-  // lanes run over centroids (C64T rows are contiguous in j), each evaluating
-  // the reference's norm in NumPy's order.  Full-scan entries sit at the back
-  // of each segment.
-  for (uint32_t g = gw; g < total; g += nw) {
-    const uint32_t sg = find_segment(pre, ql.nwaves, g);
-    const uint32_t e = g - pre[sg];
-    const QEntry* qp = queue + (size_t)sg * ql.seg + (ql.seg - 1u - e);
-    const uint32_t row = __builtin_amdgcn_readfirstlane(qp->row);
-    const float* x = X + (size_t)row * dp;
-    for (int f = lane; f < d; f += 64) xs[f] = x[f];
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    double best = 0.0;
-    int bj = -1;
-    for (int j0 = 0; j0 < k; j0 += 64) {
-      const int j = j0 + lane;
-      if (j < k) {
-        const double* ct = CT + j;
-        const double v = np_norm([&](int f) { return np_sq(ct[(size_t)f * k], xs[f]); }, d);
-        if (np_better(v, best, bj >= 0)) {
-          best = v;
-          bj = j;
-        }
-      }
-    }
-    // np.argmin across lanes: first NaN, else smallest value, lowest index
+  const int wave = threadIdx.x >> 6;
+  float* xs = xs_all + (size_t)wave * G * d;
+  const uint32_t per_batch = 8u * G;
+  for (uint32_t b0 = blockIdx.x * per_batch; b0 < total; b0 += gridDim.x * per_batch) {
+    uint32_t rows[G];
+    bool have[G];
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const double ob = __shfl_xor(best, o);
-      const int oj = __shfl_xor(bj, o);
-      bool take = false;
-      if (oj >= 0) {
-        if (bj < 0) {
-          take = true;
-        } else {
-          const bool on = ob != ob, mn = best != best;
-          take = (on && !mn) || (on == mn && (on ? oj < bj : (ob < best || (ob == best && oj < bj))));
-        }
-      }
-      if (take) {
-        best = ob;
-        bj = oj;
+    for (int g = 0; g < G; ++g) {
+      const uint32_t e = b0 + (uint32_t)(wave * G + g);
+      have[g] = e < total;
+      rows[g] = 0;
+      if (have[g]) {
+        const uint32_t sg = find_segment(pre, ql.nwaves, e);
+        const QEntry* qp = queue + (size_t)sg * ql.seg + (ql.seg - 1u - (e - pre[sg]));
+        rows[g] = __builtin_amdgcn_readfirstlane(qp->row);
+        const float* x = X + (size_t)rows[g] * dp;
+        for (int f = lane; f < d; f += 64) xs[g * d + f] = x[f];
       }
     }
-    const int lab = bj < 0 ? 0 : bj;
-    if (lane == 0) labels[row] = lab;
-    if (stats)
-      for (int f = lane; f < d; f += 64) atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)xs[f]);
-    __builtin_amdgcn_wave_barrier();  // xs reused by the next entry
+    double best[G];
+    int bj[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      best[g] = 0.0;
+      bj[g] = -1;
+    }
+    for (int c0 = 0; c0 < k; c0 += ch) {
+      __syncthreads();  // the previous chunk is consumed (and the rows staged)
+      const int cw = min(ch, k - c0);
+      for (int i = threadIdx.x; i < d * ch; i += blockDim.x) {
+        const int f = i / ch;
+        const int jj = i - f * ch;
+        sCT[i] = jj < cw ? C64T[(size_t)f * k + c0 + jj] : 0.0;
+      }
+      __syncthreads();
+      if (lane < cw) {
+        const double* ct = sCT + lane;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          if (!have[g]) continue;
+          const float* xg = xs + g * d;
+          const double v = np_norm([&](int f) { return np_sq(ct[(size_t)f * ch], xg[f]); }, d);
+          if (np_better(v, best[g], bj[g] >= 0)) {
+            best[g] = v;
+            bj[g] = c0 + lane;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (!have[g]) continue;
+      double bv = best[g];
+      int bi = bj[g];
+      // np.argmin across lanes: first NaN, else smallest value, lowest index
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const double ob = __shfl_xor(bv, o);
+        const int oj = __shfl_xor(bi, o);
+        bool take = false;
+        if (oj >= 0) {
+          if (bi < 0) {
+            take = true;
+          } else {
+            const bool on = ob != ob, mn = bv != bv;
+            take = (on && !mn) || (on == mn && (on ? oj < bi : (ob < bv || (ob == bv && oj < bi))));
+          }
+        }
+        if (take) {
+          bv = ob;
+          bi = oj;
+        }
+      }
+      const int lab = bi < 0 ? 0 : bi;
+      if (lane == 0) labels[rows[g]] = lab;
+      if (stats)
+        for (int f = lane; f < d; f += 64) atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)xs[g * d + f]);
+    }
   }
 }
 
@@ -1588,11 +1615,12 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (g.d > 256) return hipErrorInvalidValue;
-  const size_t bytes = (size_t)g.k * g.d * 8;
-  const int use_lds = bytes + FS_XS_BYTES + pre_bytes <= LDS_MAX ? 1 : 0;
-  hipLaunchKernelGGL(k_fullscan, dim3(n_cu), dim3(1024), (use_lds ? bytes : 0) + FS_XS_BYTES + pre_bytes, s, X,
-                     g.dp, g.d, g.k,
-                     C64T, queue, qcount, ql, labels, use_lds, stats);
+  constexpr int G = 4;
+  const int ch = g.d <= 128 ? 64 : 32;  // chunk columns: <= 64 KiB of LDS
+  const size_t fs_lds = (size_t)g.d * ch * 8 + (size_t)8 * G * g.d * 4 + pre_bytes;
+  if (fs_lds > LDS_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_fullscan<G>, dim3(n_cu), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T, queue, qcount, ql,
+                     labels, ch, stats);
   return hipGetLastError();
 }
 
