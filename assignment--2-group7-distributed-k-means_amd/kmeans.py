@@ -79,7 +79,8 @@ class LloydRunner:
         nonfinite = bool(st.nonfinite)
         if st.n_empty:                                         # L191
             empty = [j for j in range(k) if counts[j] == 0]
-            log(f"  WARNING: {len(empty)} empty cluster(s) detected. Reinitializing...")
+            if log:
+                log(f"  WARNING: {len(empty)} empty cluster(s) detected. Reinitializing...")
             seed = self.comm.broadcast_obj(model._empty_seed())    # int(time.time()), L196
             gidx = sampling.take_sample(self.pl.global_sizes, len(empty), seed)
             reps = self.rows(gidx) if gidx else np.zeros((0, self.pl.d))
@@ -94,21 +95,23 @@ class LloydRunner:
         if model.compute_sse:                                  # L278-286
             sse = float(st.sse)
             model.sse_history.append(sse)
-            if len(model.sse_history) > 1 and sse > model.sse_history[-2] + 1e-6:
+            if log and len(model.sse_history) > 1 and sse > model.sse_history[-2] + 1e-6:
                 log(f"  WARNING: SSE increased from {model.sse_history[-2]:.4f} to {sse:.4f}")
         if nonfinite:                                          # L289-290
             raise ValueError(f"NaN or Inf detected in centroids at iteration {iteration + 1}")
-        cluster_sizes = [int(c) for c in counts]               # L297
-        if model.compute_sse and model.sse_history:
-            log(f"Iteration {iteration + 1}: SSE = {model.sse_history[-1]:.4f}, "
-                f"Max Shift = {max_shift:.6f}, Cluster Sizes = {cluster_sizes}")
-        else:
-            log(f"Iteration {iteration + 1}: Max Shift = {max_shift:.6f}, Cluster Sizes = {cluster_sizes}")
+        if log:  # None when nothing is printed (not verbose, or not rank 0): skip the formatting
+            cluster_sizes = [int(c) for c in counts]           # L297
+            if model.compute_sse and model.sse_history:
+                log(f"Iteration {iteration + 1}: SSE = {model.sse_history[-1]:.4f}, "
+                    f"Max Shift = {max_shift:.6f}, Cluster Sizes = {cluster_sizes}")
+            else:
+                log(f"Iteration {iteration + 1}: Max Shift = {max_shift:.6f}, Cluster Sizes = {cluster_sizes}")
         eng.commit()                                           # L307
         self.last = {"max_shift": max_shift, "sse": sse, "counts": counts, "n_empty": int(st.n_empty),
                      "q_rerank": int(st.q_rerank), "q_full": int(st.q_full)}
         if max_shift < model.tolerance:                        # L310-313
-            log(f"Converged after {iteration + 1} iterations")
+            if log:
+                log(f"Converged after {iteration + 1} iterations")
             return True
         return False
 
@@ -178,10 +181,13 @@ class KMeans:
         return int(time.time())  # kmeans_spark.py:196
 
     def _log(self, comm: Communicator):
+        """The line printer of this run, or None when nothing would be printed."""
+        if not (self.verbose and comm.rank == 0):
+            return None
+
         def say(msg: str):
-            if self.verbose and comm.rank == 0:
-                print(msg)
-                sys.stdout.flush()
+            print(msg)
+            sys.stdout.flush()
         return say
 
     def _make_runner(self, rdd, comm: Communicator) -> LloydRunner:
@@ -212,8 +218,9 @@ class KMeans:
         self.centroids = self._initialize_centroids(run)       # L259
         self.sse_history = []                                  # L260
         say = self._log(comm)
-        say(f"Starting K-Means with k={self.k}, max_iter={self.max_iter}, tolerance={self.tolerance}")
-        say(f"SSE computation: {'ENABLED' if self.compute_sse else 'DISABLED (for performance)'}")
+        if say:
+            say(f"Starting K-Means with k={self.k}, max_iter={self.max_iter}, tolerance={self.tolerance}")
+            say(f"SSE computation: {'ENABLED' if self.compute_sse else 'DISABLED (for performance)'}")
         out_dtype = run.pl.dtype
         run.engine.set_centroids(np.asarray(self.centroids, dtype=np.float64))
         try:
