@@ -1634,18 +1634,23 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
 // ---------------------------------------------------------------------------
 static constexpr int STATS_LDS = 156 * 1024;
 
+// The workgroup also owns a feature range [f0, f0 + fr) (blockIdx.z):
+// splitting the features instead of the clusters keeps X read once when
+// k (d+1) doubles exceed LDS but k (fr+1) fit (c4: 1024 clusters x 16 features).
 __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int64_t n, int d, int dp, int k,
                                                 const int32_t* __restrict__ labels, double* __restrict__ stats,
-                                                int kr, int64_t rows_per_block) {
+                                                int kr, int fr, int64_t rows_per_block) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* tab = reinterpret_cast<double*>(smem);
-  // LDS row of a cluster: dp feature slots + count.  Feature f = 4m + c of a
-  // row is stored at slot c*L + m (L = dp/4 lanes per row), so the 4 atomics
-  // of a float4 each hit L consecutive doubles: no bank conflicts.
-  const int RS = dp + 1;
-  const int L = dp / 4;
+  // LDS row of a cluster: fr feature slots + count.  Feature f0 + 4m + c is
+  // stored at slot c*L + m (L = fr/4 lanes per row), so the 4 atomics of a
+  // float4 each hit L consecutive doubles: no bank conflicts.
+  const int RS = fr + 1;
+  const int L = fr / 4;
   const int c0 = blockIdx.y * kr;
   const int c1 = min(k, c0 + kr);
+  const int f0 = blockIdx.z * fr;
+  const bool counts = blockIdx.z == 0;
   const int nent = (c1 - c0) * RS;
   for (int i = threadIdx.x; i < nent; i += blockDim.x) tab[i] = 0.0;
   __syncthreads();
@@ -1661,14 +1666,15 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
   for (int64_t cr = r0 + (int64_t)wave * 64; cr < r1; cr += (int64_t)nwaves * 64) {
     const int nrow = (int)min((int64_t)64, r1 - cr);
     const int labreg = lane < nrow ? labels[cr + lane] : -1;
-    if (lane < nrow && labreg >= c0 && labreg < c1) atomicAdd(tab + (labreg - c0) * RS + dp, 1.0);  // counts
-    const float4* base = reinterpret_cast<const float4*>(X + cr * dp);
+    if (counts && lane < nrow && labreg >= c0 && labreg < c1) atomicAdd(tab + (labreg - c0) * RS + fr, 1.0);
+    const float* base = X + cr * dp + f0;
     for (int rb = 0; rb < nrow; rb += P * U) {
       float4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int rr = rb + u * P + q;
-        v[u] = rr < nrow ? base[(size_t)rr * L + mm] : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[u] = rr < nrow ? *reinterpret_cast<const float4*>(base + (size_t)rr * dp + 4 * mm)
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1692,37 +1698,56 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
     const double v = tab[i];
     if (v == 0.0) continue;
     int f;
-    if (p == dp) {
-      f = d;  // count
+    if (p == fr) {
+      f = d;  // count (feature range 0 only)
     } else {
-      f = 4 * (p % L) + p / L;
+      f = f0 + 4 * (p % L) + p / L;
       if (f >= d) continue;  // zero padding
     }
     atomicAdd(stats + (size_t)(c0 + j) * d1 + f, v);
   }
 }
 
+// features per range: the widest (fewest blocks, longest row segments) among
+// those needing the fewest cluster ranges; segments stay >= 64 bytes
+static void stats_ranges(const Geometry& g, int* fr_out, int* kr_out) {
+  int best_fr = g.dp, best_kr = 0, best_ncr = 1 << 30;
+  for (int fr = g.dp; fr >= 16 && g.dp % fr == 0 && fr % 4 == 0; fr /= 2) {
+    int kr = (int)(STATS_LDS / ((size_t)(fr + 1) * 8));
+    if (kr > g.k) kr = g.k;
+    const int ncr = (g.k + kr - 1) / kr;
+    if (ncr < best_ncr) {
+      best_ncr = ncr;
+      best_fr = fr;
+      best_kr = kr;
+    }
+    if (fr % 8) break;
+  }
+  *fr_out = best_fr;
+  *kr_out = best_kr;
+}
+
 hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels, double* stats, int n_cu,
                         hipStream_t s) {
   if (g.n == 0) return hipSuccess;
-  const int RS = g.dp + 1;
   if (g.dp > 256 || g.dp % 4) return hipErrorInvalidValue;
-  int kr = (int)(STATS_LDS / ((size_t)RS * 8));
+  int fr = 0, kr = 0;
+  stats_ranges(g, &fr, &kr);
   if (kr < 1) return hipErrorInvalidValue;
-  if (kr > g.k) kr = g.k;
   const int ranges = (g.k + kr - 1) / kr;
-  const size_t lds = (size_t)kr * RS * 8;
+  const int franges = g.dp / fr;
+  const size_t lds = (size_t)kr * (fr + 1) * 8;
   int per_cu = (int)((160 * 1024) / (lds + 1024));
   if (per_cu < 1) per_cu = 1;
   if (per_cu > 2) per_cu = 2;
-  int64_t bx = (int64_t)n_cu * per_cu / ranges;
+  int64_t bx = (int64_t)n_cu * per_cu / (ranges * franges);
   if (bx < 1) bx = 1;
   const int64_t min_rows = 4096;
   if (bx > (g.n + min_rows - 1) / min_rows) bx = (g.n + min_rows - 1) / min_rows;
   int64_t rpb = (g.n + bx - 1) / bx;
   rpb = (rpb + 63) / 64 * 64;
-  hipLaunchKernelGGL(k_stats, dim3((unsigned)bx, (unsigned)ranges), dim3(1024), lds, s, X, g.n, g.d, g.dp, g.k,
-                     labels, stats, kr, rpb);
+  hipLaunchKernelGGL(k_stats, dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024), lds, s, X, g.n,
+                     g.d, g.dp, g.k, labels, stats, kr, fr, rpb);
   return hipGetLastError();
 }
 
@@ -1871,8 +1896,10 @@ size_t sorted_stats_words(int64_t n, int k) { return 2 * (size_t)n + 3 * (size_t
 // label/permutation traffic, and cursor atomics that contend when k is small)
 // is cheaper
 bool stats_needs_sort(const Geometry& g) {
-  const size_t kr = (size_t)STATS_LDS / ((size_t)(g.dp + 1) * 8);
-  return kr == 0 || ((size_t)g.k + kr - 1) / kr >= 3;
+  static const int min_ranges = small_env("KM_SORT_MIN_RANGES", 3);  // A/B knob
+  int fr = 0, kr = 0;
+  stats_ranges(g, &fr, &kr);
+  return kr == 0 || (g.k + kr - 1) / kr >= min_ranges;
 }
 
 hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t* labels, double* stats,

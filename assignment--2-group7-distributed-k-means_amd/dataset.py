@@ -120,13 +120,17 @@ class LocalContext:
 class DeviceBlobs:
     """Synthetic Gaussian blobs (centers uniform in (-box, box), std ``std``)
     generated in HBM by a counter-based generator keyed on the global row, so
-    the data are identical for any sharding.  ``n`` is the GLOBAL row count."""
+    the data are identical for any sharding.  ``n`` is the GLOBAL row count;
+    ``partitions`` is the dataset's partition layout for ``takeSample`` (like
+    ``sc.parallelize(X, partitions)``), independent of how many GPUs hold it,
+    so the initial centroids and the whole run are the same on 1..8 GPUs."""
     n: int
     d: int
     n_centers: int
     box: float = 10.0
     std: float = 1.0
     seed: int = 0
+    partitions: int = 8
 
 
 @dataclass
@@ -173,7 +177,9 @@ def place(rdd, comm) -> Placement:
         W, r = comm.world, comm.rank
         sizes = [((i + 1) * rdd.n) // W - (i * rdd.n) // W for i in range(W)]
         row0 = (r * rdd.n) // W
-        return Placement(global_sizes=sizes, local_rows=None, row0=row0, n_local=sizes[r], n_global=rdd.n,
+        P = max(1, int(rdd.partitions))
+        layout = [((i + 1) * rdd.n) // P - (i * rdd.n) // P for i in range(P)]
+        return Placement(global_sizes=layout, local_rows=None, row0=row0, n_local=sizes[r], n_global=rdd.n,
                          d=rdd.d, dtype=np.float64, blobs=rdd)
     parts = _partitions_of(rdd)
     d = None

@@ -90,23 +90,44 @@ def _bernoulli_pass_py(partition_sizes: Sequence[int], fraction: float, seed: in
     return picked
 
 
-def _bernoulli_pass(partition_sizes: Sequence[int], fraction: float, seed: int) -> List[int]:
+def _partition_picks(split: int, base: int, size: int, fraction: float, seed: int) -> np.ndarray:
+    """Global indices of one partition's Bernoulli sample (its own stream)."""
+    rs = _python_random_stream(seed ^ split)
+    chunk = 1 << 24
+    out = []
+    for s in range(0, size, chunk):
+        u = rs.random_sample(min(chunk, size - s))   # releases the GIL: partitions run in parallel threads
+        out.append(np.nonzero(u < fraction)[0] + (base + s))
+    return np.concatenate(out) if out else np.zeros(0, dtype=np.int64)
+
+
+def _bernoulli_pass(partition_sizes: Sequence[int], fraction: float, seed: int, comm=None) -> List[int]:
+    """Every partition's picks in partition order.  The partitions are
+    independent streams (seed ^ split): they are split over the ranks of
+    ``comm`` (partition p on rank p % world, results all-gathered) and over
+    host threads within a rank; the result does not depend on either."""
     if sum(partition_sizes) <= 65536:
         return _bernoulli_pass_py(partition_sizes, fraction, seed)
-    picked = []
-    base = 0
-    chunk = 1 << 24
-    for split, size in enumerate(partition_sizes):
-        rs = _python_random_stream(seed ^ split)
-        for s in range(0, size, chunk):
-            u = rs.random_sample(min(chunk, size - s))
-            picked.append(np.nonzero(u < fraction)[0] + (base + s))
-        base += size
-    return np.concatenate(picked).tolist() if picked else []
+    bases = np.concatenate([[0], np.cumsum(partition_sizes)[:-1]]).astype(np.int64)
+    world = comm.world if comm is not None else 1
+    rank = comm.rank if comm is not None else 0
+    mine = [p for p in range(len(partition_sizes)) if p % world == rank and partition_sizes[p] > 0]
+    if len(mine) > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=min(len(mine), 16)) as ex:
+            parts = list(ex.map(lambda p: _partition_picks(p, int(bases[p]), int(partition_sizes[p]), fraction,
+                                                           seed), mine))
+    else:
+        parts = [_partition_picks(p, int(bases[p]), int(partition_sizes[p]), fraction, seed) for p in mine]
+    local = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int64)
+    if world > 1:
+        local = np.concatenate(comm.allgather_array(local.astype(np.int64)))
+    return np.sort(local, kind="stable").tolist()
 
 
-def take_sample(partition_sizes: Sequence[int], num: int, seed: Optional[int]) -> List[int]:
-    """Global row indices that ``takeSample(False, num, seed)`` returns, in order."""
+def take_sample(partition_sizes: Sequence[int], num: int, seed: Optional[int], comm=None) -> List[int]:
+    """Global row indices that ``takeSample(False, num, seed)`` returns, in order.
+    With ``comm`` every rank must call it with the same arguments."""
     if num < 0:
         raise ValueError("Sample size cannot be negative.")
     total = int(sum(partition_sizes))
@@ -114,15 +135,17 @@ def take_sample(partition_sizes: Sequence[int], num: int, seed: Optional[int]) -
         return []
     if seed is None:
         seed = random.randint(0, sys.maxsize)
+        if comm is not None and comm.world > 1:
+            seed = comm.broadcast_obj(seed)
     rand = random.Random(seed)
     if num >= total:
         idx = list(range(total))
         rand.shuffle(idx)
         return idx
     fraction = _fraction(num, total)
-    samples = _bernoulli_pass(partition_sizes, fraction, seed)
+    samples = _bernoulli_pass(partition_sizes, fraction, seed, comm)
     while len(samples) < num:
         seed = rand.randint(0, sys.maxsize)
-        samples = _bernoulli_pass(partition_sizes, fraction, seed)
+        samples = _bernoulli_pass(partition_sizes, fraction, seed, comm)
     rand.shuffle(samples)
     return samples[0:num]

@@ -133,6 +133,7 @@ def _check_labels(X, C, labels):
     (40, 64, 36, 8),           # two 32-point tiles, the second partial (fused kernel tail)
     (1000, 40, 70, 10),        # d=40 -> 48 padded (fused <3,4>, generic row norms)
     (5000, 64, 300, 60),       # k=300 -> kp=320: unfused MFMA path + LDS-range statistics
+    (6000, 128, 1200, 100),    # statistics tiled over 2 cluster ranges x 8 feature ranges
 ])
 def test_one_step_vs_oracle(n, d, k, centers):
     X = _blobs(n, d, centers, seed=n + d + k)

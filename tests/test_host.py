@@ -84,9 +84,11 @@ def test_placement_partitions_and_order():
     pa = [place(X, FakeComm(r, 3)) for r in range(3)]
     assert pa[0].global_sizes == [1000]
     np.testing.assert_array_equal(np.concatenate([p.local_rows for p in pa]), X)
-    # device blobs: row split only
-    pb = place(ka.DeviceBlobs(n=10, d=4, n_centers=2), FakeComm(1, 3))
-    assert (pb.row0, pb.n_local, pb.global_sizes) == (3, 3, [3, 3, 4])
+    # device blobs: rows split over the ranks; the takeSample layout is the
+    # dataset's own partitioning, the same for any number of ranks
+    pb = place(ka.DeviceBlobs(n=10, d=4, n_centers=2, partitions=4), FakeComm(1, 3))
+    assert (pb.row0, pb.n_local, pb.global_sizes) == (3, 3, [2, 3, 2, 3])
+    assert place(ka.DeviceBlobs(n=10, d=4, n_centers=2, partitions=4), FakeComm(0, 1)).global_sizes == [2, 3, 2, 3]
 
 
 def test_parallelize_slices_like_pyspark():
@@ -201,3 +203,41 @@ def test_two_ranks_gloo_match_single_rank(golden, name):
         np.testing.assert_allclose(sse, g["sse_history"], rtol=1e-9)
         np.testing.assert_array_equal(labels, g["labels"])
     assert res[0][4] and not res[1][4]  # only rank 0 logs, like the single driver
+
+
+def _sample_rank_main(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kmeans_amd import sampling
+        from kmeans_amd.comm import Communicator
+        comm = Communicator()
+        sizes = [40000, 30000, 0, 50001, 25000]
+        q.put((rank, sampling.take_sample(sizes, 37, 2024, comm), sampling.take_sample(sizes, 5, 7, comm)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_take_sample_split_over_ranks_is_identical():
+    # partitions are independent streams: splitting them over ranks (and host
+    # threads) must not change takeSample's answer (kmeans_spark.py:72, :196)
+    import torch.multiprocessing as mp
+    from kmeans_amd import sampling
+    sizes = [40000, 30000, 0, 50001, 25000]
+    want = (sampling.take_sample(sizes, 37, 2024), sampling.take_sample(sizes, 5, 7))
+    assert want[0] == orc.take_sample_indices(sizes, 37, 2024)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sample_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for _, a, b in res:
+        assert (a, b) == want
