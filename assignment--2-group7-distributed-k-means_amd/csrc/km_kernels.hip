@@ -398,8 +398,11 @@ struct MfmaArgs {
 // 32b + (l&31), features 16t + 8(l>>5) .. +8): lane-linear, bank-conflict
 // free, and every read of a block is base + immediate offset.
 // ABL (diagnostic builds only, never selected by default): 1 = no key
-// updates, 2 = no MFMAs (labels are then wrong; timing only)
-template <int NS, int WAVES, int ABL = 0>
+// updates, 2 = no MFMAs (labels are then wrong; timing only).
+// T2: chains keep their best two keys (3 VALU per score instead of 4; for
+// small d, where the key updates, not the MFMAs, bound the loop); a point
+// whose best two share a chain then has no re-rank certificate (full scan).
+template <int NS, int WAVES, int ABL = 0, bool T2 = false>
 __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_assign_mfma(MfmaArgs A) {
   constexpr int DP = 16 * NS;
   constexpr int BLKB = NS * 1024;  // bytes of one block's fragments (one of hi / lo)
@@ -535,7 +538,14 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
         return;
       }
       const float key = __uint_as_float((__float_as_uint(acc[reg]) & ~maskq) | jg[reg >> 2]);
-      top3_insert(a1[reg & 3], a2[reg & 3], a3[reg & 3], key);
+      if constexpr (T2) {
+        const int c = reg & 3;
+        const float n1 = __builtin_amdgcn_fmed3f(a1[c], key, -FLT_MAX);
+        a2[c] = __builtin_amdgcn_fmed3f(a1[c], a2[c], key);
+        a1[c] = n1;
+      } else {
+        top3_insert(a1[reg & 3], a2[reg & 3], a3[reg & 3], key);
+      }
     };
     // MFMAs of block `blk` into `cur` while the 16 key updates of the
     // previous block (`prev`, index words already in jg) fill the gaps.  A
@@ -593,7 +603,9 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
     for (int c = 0; c < 4; ++c) {
       top3p_insert(k1, k2, k3, p1, p2, a1[c], ((__float_as_uint(a1[c]) & maskq) << 2) | (uint32_t)c);
       top3p_insert(k1, k2, k3, p1, p2, a2[c], ((__float_as_uint(a2[c]) & maskq) << 2) | (uint32_t)c);
-      top3p_insert(k1, k2, k3, p1, p2, a3[c], 0u);  // a 3rd never enters the top two
+      // a 3rd never enters the top two; with T2 the chain's dropped keys are
+      // only known to be >= its second, which stands in for its third
+      top3p_insert(k1, k2, k3, p1, p2, T2 ? a2[c] : a3[c], 0u);
     }
     {  // the two lane halves hold disjoint centroid rows of the same point
       const float q1 = __shfl_xor(k1, 32), q2 = __shfl_xor(k2, 32), q3 = __shfl_xor(k3, 32);
@@ -613,10 +625,16 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
     // negated tests: NaN (non-finite data) falls through to the full float64
     // scan, whose np.argmin semantics then pick the first index
     uint32_t kind = 0;
-    if (!(k3 - k1 > thr3))
-      kind = 2;
-    else if (!(k2 - k1 > thr2))
-      kind = 1;
+    if constexpr (T2) {
+      // p1, p2 in one chain (same j & 7): no certificate for the pair
+      const bool same_chain = ((p1 ^ p2) & 7u) == 0u;
+      if (!(k2 - k1 > thr2)) kind = (same_chain || !(k3 - k1 > thr3)) ? 2u : 1u;
+    } else {
+      if (!(k3 - k1 > thr3))
+        kind = 2;
+      else if (!(k2 - k1 > thr2))
+        kind = 1;
+    }
     const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
     if (h == 0 && valid) A.labels[row] = lab;
     const bool enq = (h == 0) && valid && (kind != 0);
@@ -684,8 +702,24 @@ hipError_t launch_prep_split(const float* C32, const Geometry& g, const float* c
   return hipGetLastError();
 }
 
+static int mfma_top2(int ns) {
+  static const int e = small_env("KM_TOP2", -1);  // -1: by d (key-update-bound shapes), 0/1: force
+  return e >= 0 ? e : (ns <= 2 ? 1 : 0);
+}
+
 template <int NS>
 static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, const MfmaArgs& a) {
+  if constexpr (NS <= 4) {
+    if (mfma_top2(NS)) {
+      if (waves == 4)
+        hipLaunchKernelGGL((k_assign_mfma<NS, 4, 0, true>), dim3(blocks), dim3(256), lds, s, a);
+      else if (waves == 12)
+        hipLaunchKernelGGL((k_assign_mfma<NS, 12, 0, true>), dim3(blocks), dim3(768), lds, s, a);
+      else
+        hipLaunchKernelGGL((k_assign_mfma<NS, 8, 0, true>), dim3(blocks), dim3(512), lds, s, a);
+      return;
+    }
+  }
   if constexpr (NS >= 12) {
     hipLaunchKernelGGL((k_assign_mfma<NS, 4>), dim3(blocks), dim3(256), lds, s, a);
   } else {

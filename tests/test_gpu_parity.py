@@ -194,6 +194,8 @@ def test_predict_requires_fit():
     (20000, 64, 127, 127),   # fused kernel, duplicates on other chains -> pair re-rank
     (20000, 16, 12, 12),     # small path (k <= 32): in-thread re-rank / full scan
     (8000, 100, 150, 150),   # unfused MFMA path (kp = 320)
+    (8000, 32, 300, 300),    # unfused, top-2 chains (d <= 32), duplicates on other chains -> re-rank
+    (8000, 32, 264, 264),    # unfused, top-2 chains, duplicates on the same chain -> full scans
     (6000, 200, 40, 40),     # d = 200: pairwise split 96 + 104
     (6000, 250, 20, 20),     # d = 250: split 120 + (64 + 66), two levels
 ])
