@@ -72,7 +72,7 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
                           double* stats, int n_cu, hipStream_t s);
 // Fused assign + partial sums (kp*dp <= 16384 class): fp16 hi image in VGPRs,
 // lo image + float64 sum table in LDS; decided points summed here, queued
-// points by launch_resolve(stats), sizes by launch_count.
+// points (and their counts) by launch_resolve(stats).
 bool fused_path_ok(const Geometry& g);
 void dump_fused_stamps();  // diagnostic (KM_ABLATE=7)
 hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, const _Float16* Chi,
@@ -82,7 +82,6 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
 hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float* cabs, int dp, float* bnd,
                                hipStream_t s);
 hipError_t launch_row_norm(const float* X, const Geometry& g, float* xnorm, hipStream_t s);
-hipError_t launch_count(const int32_t* labels, const Geometry& g, double* stats, int n_cu, hipStream_t s);
 // large k: counting sort of the labels + per-cluster float64 row sums (X read
 // once); scratch = sorted_stats_words(n, k) uint32 words
 bool stats_needs_sort(const Geometry& g);

@@ -814,7 +814,7 @@ hipError_t launch_absmax(const float* X, int64_t nfloats, float* out, hipStream_
 // (score | j>>2), merged to the top-3 values and the best two indices, the
 // rigorous screening bound, label + ambiguous-point queue, and for every
 // decided point its exact fp32 row added to the table.  Ambiguous points are
-// added by the resolver kernels, counts by k_count over the final labels.
+// added by the resolver kernels (with their counts).
 // The table is flushed with one float64 atomic per non-zero entry.
 // ---------------------------------------------------------------------------
 
@@ -861,7 +861,7 @@ struct FusedArgs {
   int32_t* labels;
   QEntry* queue;
   uint32_t* qcount;
-  double* stats;       // [k][d+1] (sums; counts by k_count)
+  double* stats;       // [k][d+1] (sums, counts)
 };
 
 constexpr int ceil_log2_c(int v) { return v <= 1 ? 0 : 1 + ceil_log2_c((v + 1) / 2); }
@@ -896,7 +896,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   const int h = lane >> 5;
   for (int i = threadIdx.x; i < KP; i += WAVES * 64) sCn[i] = A.cn2s[i];
   if constexpr (STATS)
-    for (int i = threadIdx.x; i < DP * KP; i += WAVES * 64) tab[i] = 0.0;
+    for (int i = threadIdx.x; i < (DP + 1) * KP; i += WAVES * 64) tab[i] = 0.0;
   f16x8 Ahi[NB][NS], Alo[NB][NS];
 #pragma unroll
   for (int b = 0; b < NB; ++b)
@@ -1146,6 +1146,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) atomicAdd(tp + (size_t)(16 * t + e) * KP, (double)xe[e]);
         }
+        if (h == 0) atomicAdd(tab + (size_t)DP * KP + lab, 1.0);  // count row
       }
     }
     if constexpr (ABL == 7) {
@@ -1183,11 +1184,11 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
     const int d1 = A.d + 1;
     // row-major walk of the global [k][d+1] buffer: a wave's atomics cover
     // contiguous bytes (scattered float64 atomics run ~17x slower)
-    for (int i = threadIdx.x; i < DP * KP; i += WAVES * 64) {
-      const int j = i / DP;
-      const int f = i - j * DP;
+    for (int i = threadIdx.x; i < (DP + 1) * KP; i += WAVES * 64) {
+      const int j = i / (DP + 1);
+      const int f = i - j * (DP + 1);
       const double v = tab[(size_t)f * KP + j];
-      if (v != 0.0 && f < A.d && j < A.k) atomicAdd(A.stats + (size_t)j * d1 + f, v);
+      if (v != 0.0 && (f < A.d || f == DP) && j < A.k) atomicAdd(A.stats + (size_t)j * d1 + (f == DP ? A.d : f), v);
     }
   }
 }
@@ -1259,22 +1260,6 @@ __global__ __launch_bounds__(256) void k_row_norm_any(const float* __restrict__ 
   }
 }
 
-// cluster sizes from the final labels into the count column of stats
-__global__ __launch_bounds__(1024) void k_count(const int32_t* __restrict__ labels, int64_t n, int k,
-                                                double* __restrict__ stats, int d) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
-  for (int i = threadIdx.x; i < k; i += blockDim.x) hist[i] = 0u;
-  __syncthreads();
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int l = labels[i];
-    if ((unsigned)l < (unsigned)k) atomicAdd(hist + l, 1u);
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < k; i += blockDim.x)
-    if (hist[i]) atomicAdd(stats + (size_t)i * (d + 1) + d, (double)hist[i]);
-}
-
 // diagnostic: print and clear the ABL=7 phase stamps (cycles summed over waves)
 void dump_fused_stamps() {
   unsigned long long v[8];
@@ -1329,7 +1314,7 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
   ql->seg = seg;
   ql->nwaves = (uint32_t)nw;
   FusedArgs a{X, xnorm, g.n, g.k, g.d, seg, ChiF, CloF, cn2s, bnd, xabs, cabs, labels, queue, qcount, stats};
-  const size_t lds = (size_t)g.kp * 4 + (with_stats ? (size_t)g.dp * g.kp * 8 : 0);
+  const size_t lds = (size_t)g.kp * 4 + (with_stats ? (size_t)(g.dp + 1) * g.kp * 8 : 0);
 #define KM_FUSED_CASE(NS_, NB_)                                                                        \
   case NS_ * 100 + NB_:                                                                                \
     if (with_stats)                                                                                    \
@@ -1385,14 +1370,6 @@ hipError_t launch_row_norm(const float* X, const Geometry& g, float* xnorm, hipS
     case 64: hipLaunchKernelGGL(k_row_norm<64>, grid, blk, 0, s, X, g.n, xnorm); break;
     default: hipLaunchKernelGGL(k_row_norm_any, grid, blk, 0, s, X, g.n, g.dp, xnorm); break;
   }
-  return hipGetLastError();
-}
-
-hipError_t launch_count(const int32_t* labels, const Geometry& g, double* stats, int n_cu, hipStream_t s) {
-  if (g.n == 0) return hipSuccess;
-  int64_t blocks = (g.n + 1023) / 1024;
-  if (blocks > n_cu) blocks = n_cu;
-  hipLaunchKernelGGL(k_count, dim3((unsigned)blocks), dim3(1024), (size_t)g.k * 4, s, labels, g.n, g.k, stats, g.d);
   return hipGetLastError();
 }
 
@@ -1469,9 +1446,9 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
                                                   int tab_kp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* tab = reinterpret_cast<double*>(smem);
-  uint32_t* pre = reinterpret_cast<uint32_t*>(smem + (stats && tab_kp ? (size_t)d * tab_kp * 8 : 0));
+  uint32_t* pre = reinterpret_cast<uint32_t*>(smem + (stats && tab_kp ? (size_t)(d + 1) * tab_kp * 8 : 0));
   if (stats && tab_kp)
-    for (int i = threadIdx.x; i < d * tab_kp; i += blockDim.x) tab[i] = 0.0;
+    for (int i = threadIdx.x; i < (d + 1) * tab_kp; i += blockDim.x) tab[i] = 0.0;
   block_prefix(qcount, 0, ql.nwaves, pre);
   const uint32_t total = pre[ql.nwaves];
   const int u = threadIdx.x & 7;
@@ -1520,13 +1497,19 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
         else
           atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)x[f]);
       }
+      if (u == 0) {  // count
+        if (tab_kp)
+          atomicAdd(tab + (size_t)d * tab_kp + lab, 1.0);
+        else
+          atomicAdd(stats + (size_t)lab * (d + 1) + d, 1.0);
+      }
     }
   }
   if (stats && tab_kp) {
     __syncthreads();
-    for (int i = threadIdx.x; i < d * tab_kp; i += blockDim.x) {
-      const int j = i / d;
-      const int f = i - j * d;
+    for (int i = threadIdx.x; i < (d + 1) * tab_kp; i += blockDim.x) {
+      const int j = i / (d + 1);
+      const int f = i - j * (d + 1);
       const double v = tab[(size_t)f * tab_kp + j];
       if (v != 0.0 && j < k) atomicAdd(stats + (size_t)j * (d + 1) + f, v);
     }
@@ -1629,8 +1612,10 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
       }
       const int lab = bi < 0 ? 0 : bi;
       if (lane == 0) labels[rows[g]] = lab;
-      if (stats)
+      if (stats) {
         for (int f = lane; f < d; f += 64) atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)xs[g * d + f]);
+        if (lane == 0) atomicAdd(stats + (size_t)lab * (d + 1) + d, 1.0);  // count
+      }
     }
   }
 }
@@ -1642,7 +1627,7 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   constexpr size_t LDS_MAX = 160 * 1024;
   const size_t pre_bytes = ((size_t)ql.nwaves + 1) * 4;
   if (pre_bytes > LDS_MAX / 2) return hipErrorInvalidValue;
-  const size_t tab_bytes = (size_t)g.d * g.kp * 8;
+  const size_t tab_bytes = (size_t)(g.d + 1) * g.kp * 8;
   const int tab_kp = (stats && tab_bytes + pre_bytes <= LDS_MAX) ? g.kp : 0;
   hipLaunchKernelGGL(k_rerank2, dim3(n_cu), dim3(1024), (tab_kp ? tab_bytes : 0) + pre_bytes, s, X, g.dp, g.d, g.k,
                      C64, queue, qcount, ql, labels, stats, tab_kp);

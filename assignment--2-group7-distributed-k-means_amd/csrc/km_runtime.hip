@@ -237,11 +237,7 @@ int run_assign(km_ctx* c, bool with_stats) {
       KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels,
                                 with_stats ? c->stats : nullptr, c->n_cu, c->stream));
     }
-    if (with_stats) {
-      ProfScope ps(c, KM_K_STATS);
-      KM_HIP(km::launch_count(c->labels, g, c->stats, c->n_cu, c->stream));
-    }
-    return KM_OK;
+    return KM_OK;  // counts are part of the fused and resolver statistics
   }
   {
     ProfScope ps(c, KM_K_ASSIGN);
