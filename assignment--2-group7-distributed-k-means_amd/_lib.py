@@ -69,6 +69,8 @@ SIGNATURES = {
     "km_replace_rows": [_P, _PI32, _PD, _I32],
     "km_commit": [_P],
     "km_gather_rows": [_P, _PI64, _I32, _PD],
+    "km_bernoulli_sample": [_P, ctypes.POINTER(ctypes.c_uint64), _PI64, _PI64, _I32, ctypes.c_double, _PI64,
+                            ctypes.c_int64, _PI64],
     "km_predict": [_P, _PI32],
     "km_labels": [_P, _PI32],
     "km_profile": [_P, _I32],

@@ -97,6 +97,9 @@ hipError_t launch_sum_x(const float* X, const Geometry& g, double* out, hipStrea
 hipError_t launch_sq_dev(const float* X, const Geometry& g, const double* mu, double* out, hipStream_t s);
 hipError_t launch_gather_rows(const float* X, const Geometry& g, const int64_t* idx, int32_t n, double* out,
                               hipStream_t s);
+// takeSample's Bernoulli pass, one wave per partition (km_sample.hip)
+hipError_t launch_bernoulli(const uint64_t* seeds, const int64_t* sizes, const int64_t* bases, int nparts,
+                            double fraction, int64_t* out, int cp, int32_t* counts, hipStream_t s);
 hipError_t launch_gen_blobs(float* X, const Geometry& g, int64_t row_offset, int32_t n_centers, float box,
                             float stddev, uint64_t seed, hipStream_t s);
 

@@ -601,6 +601,58 @@ int km_gather_rows(km_ctx* c, const int64_t* idx, int32_t n, double* out) {
   return KM_OK;
 }
 
+int km_bernoulli_sample(km_ctx* c, const uint64_t* seeds, const int64_t* sizes, const int64_t* bases, int32_t nparts,
+                        double fraction, int64_t* out, int64_t cap, int64_t* n_out) {
+  KM_REQUIRE(c && n_out, KM_ERR_ARG, "km_bernoulli_sample: null arg");
+  *n_out = 0;
+  if (nparts <= 0) return KM_OK;
+  KM_REQUIRE(seeds && sizes && bases && (cap == 0 || out), KM_ERR_ARG, "km_bernoulli_sample: null arg");
+  int64_t maxs = 0;
+  for (int i = 0; i < nparts; ++i) {
+    KM_REQUIRE(sizes[i] >= 0, KM_ERR_ARG, "km_bernoulli_sample: negative partition size");
+    maxs = std::max(maxs, sizes[i]);
+  }
+  KM_REQUIRE(fraction >= 0.0 && fraction <= 1.0, KM_ERR_ARG, "km_bernoulli_sample: fraction out of [0, 1]");
+  // per-partition slots: 4x the expected picks + 64 (more -> KM_ERR_ARG, the
+  // caller falls back to its host sampler)
+  const double expect = fraction * (double)maxs;
+  KM_REQUIRE(expect * 4.0 + 64.0 < (double)(1 << 24), KM_ERR_ARG, "km_bernoulli_sample: sample too large for the device pass");
+  const int cp = (int)(expect * 4.0) + 64;
+  KM_HIP(hipSetDevice(c->device));
+  const size_t bytes_in = (sizeof(uint64_t) + 2 * sizeof(int64_t)) * (size_t)nparts;
+  const size_t bytes_out = sizeof(int64_t) * (size_t)nparts * cp + sizeof(int32_t) * (size_t)nparts;
+  char* dbuf = nullptr;
+  KM_HIP(hipMalloc(&dbuf, bytes_in + bytes_out));
+  uint64_t* dseeds = reinterpret_cast<uint64_t*>(dbuf);
+  int64_t* dsizes = reinterpret_cast<int64_t*>(dseeds + nparts);
+  int64_t* dbases = dsizes + nparts;
+  int64_t* dout = dbases + nparts;
+  int32_t* dcounts = reinterpret_cast<int32_t*>(dout + (size_t)nparts * cp);
+  std::vector<int64_t> hout((size_t)nparts * cp);
+  std::vector<int32_t> hcounts(nparts);
+  hipError_t e = hipMemcpyAsync(dseeds, seeds, sizeof(uint64_t) * nparts, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dsizes, sizes, sizeof(int64_t) * nparts, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dbases, bases, sizeof(int64_t) * nparts, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = km::launch_bernoulli(dseeds, dsizes, dbases, nparts, fraction, dout, cp, dcounts, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(hcounts.data(), dcounts, sizeof(int32_t) * nparts, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(hout.data(), dout, sizeof(int64_t) * (size_t)nparts * cp, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(dbuf);
+  if (e != hipSuccess) return fail(KM_ERR_HIP, std::string("km_bernoulli_sample: ") + hipGetErrorString(e));
+  int64_t total = 0;
+  for (int i = 0; i < nparts; ++i) {
+    KM_REQUIRE(hcounts[i] <= cp, KM_ERR_ARG, "km_bernoulli_sample: more picks than the device pass holds");
+    total += hcounts[i];
+  }
+  KM_REQUIRE(total <= cap, KM_ERR_ARG, "km_bernoulli_sample: output capacity too small");
+  int64_t o = 0;
+  for (int i = 0; i < nparts; ++i)
+    for (int j = 0; j < hcounts[i]; ++j) out[o++] = hout[(size_t)i * cp + j];
+  *n_out = total;
+  return KM_OK;
+}
+
 int km_predict(km_ctx* c, int32_t* labels_out) {
   KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_predict: set centroids first");
   KM_REQUIRE(c->path != 0, KM_ERR_UNSUPPORTED, "km_predict: unsupported geometry");

@@ -123,14 +123,15 @@ class DeviceBlobs:
     the data are identical for any sharding.  ``n`` is the GLOBAL row count;
     ``partitions`` is the dataset's partition layout for ``takeSample`` (like
     ``sc.parallelize(X, partitions)``), independent of how many GPUs hold it,
-    so the initial centroids and the whole run are the same on 1..8 GPUs."""
+    so the initial centroids and the whole run are the same on 1..8 GPUs; the
+    Bernoulli pass runs one GPU wave per partition (km_bernoulli_sample)."""
     n: int
     d: int
     n_centers: int
     box: float = 10.0
     std: float = 1.0
     seed: int = 0
-    partitions: int = 8
+    partitions: int = 256
 
 
 @dataclass

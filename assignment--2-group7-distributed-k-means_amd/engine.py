@@ -153,6 +153,24 @@ class HipEngine:
                     "km_gather_rows")
         return out
 
+    def bernoulli(self, seeds, sizes, bases, fraction: float) -> Optional[np.ndarray]:
+        """takeSample's Bernoulli pass on this GPU (km_bernoulli_sample): the
+        picks (global row indices, partitions in the given order), or None when
+        the device pass cannot hold them (the caller samples on the host)."""
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+        sizes = np.ascontiguousarray(sizes, dtype=np.int64)
+        bases = np.ascontiguousarray(bases, dtype=np.int64)
+        cap = int(4.0 * fraction * float(sizes.sum())) + 64 * max(len(sizes), 1)
+        out = np.empty(cap, dtype=np.int64)
+        n = ctypes.c_int64(0)
+        rc = self.lib.km_bernoulli_sample(self.ctx, seeds.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                          _ptr(sizes, _PI64), _ptr(bases, _PI64), len(sizes), float(fraction),
+                                          _ptr(out, _PI64), cap, ctypes.byref(n))
+        if rc == -1:  # KM_ERR_ARG: more picks than the device pass holds
+            return None
+        self._c(rc, "km_bernoulli_sample")
+        return out[:n.value].copy()
+
     def predict(self) -> np.ndarray:
         out = np.empty(self.n, dtype=np.int32)
         self._c(self.lib.km_predict(self.ctx, _ptr(out, _PI32)), "km_predict")

@@ -40,6 +40,8 @@ class LloydRunner:
         self.comm = comm
         self.k = k
         self.last = None
+        # takeSample's Bernoulli pass on the GPU when the engine has one
+        self.sampler = getattr(engine, "bernoulli", None)
 
     # -- set-up --------------------------------------------------------------------
     def load(self) -> None:
@@ -82,7 +84,7 @@ class LloydRunner:
             if log:
                 log(f"  WARNING: {len(empty)} empty cluster(s) detected. Reinitializing...")
             seed = self.comm.broadcast_obj(model._empty_seed())    # int(time.time()), L196
-            gidx = sampling.take_sample(self.pl.global_sizes, len(empty), seed, self.comm)
+            gidx = sampling.take_sample(self.pl.global_sizes, len(empty), seed, self.comm, self.sampler)
             reps = self.rows(gidx) if gidx else np.zeros((0, self.pl.d))
             old = eng.get_centroids(0)
             ids = empty[:len(reps)]                            # the rest keep the old centroid (L204)
@@ -200,7 +202,7 @@ class KMeans:
 
     def _initialize_centroids(self, run: LloydRunner) -> np.ndarray:
         """kmeans_spark.py:58-82: k distinct rows by the takeSample policy."""
-        gidx = sampling.take_sample(run.pl.global_sizes, self.k, self.seed, run.comm)
+        gidx = sampling.take_sample(run.pl.global_sizes, self.k, self.seed, run.comm, run.sampler)
         if len(gidx) < self.k:
             raise ValueError(f"Not enough data points ({len(gidx)}) to initialize {self.k} clusters")
         centroids = np.array(run.rows(gidx))

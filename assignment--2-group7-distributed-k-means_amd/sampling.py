@@ -101,23 +101,31 @@ def _partition_picks(split: int, base: int, size: int, fraction: float, seed: in
     return np.concatenate(out) if out else np.zeros(0, dtype=np.int64)
 
 
-def _bernoulli_pass(partition_sizes: Sequence[int], fraction: float, seed: int, comm=None) -> List[int]:
+def _bernoulli_pass(partition_sizes: Sequence[int], fraction: float, seed: int, comm=None,
+                    device=None) -> List[int]:
     """Every partition's picks in partition order.  The partitions are
     independent streams (seed ^ split): they are split over the ranks of
-    ``comm`` (partition p on rank p % world, results all-gathered) and over
-    host threads within a rank; the result does not depend on either."""
+    ``comm`` (partition p on rank p % world, results all-gathered), and run
+    on this rank's GPU (``device`` = HipEngine.bernoulli, one wave per
+    partition) or else over host threads; the result does not depend on
+    any of that."""
     if sum(partition_sizes) <= 65536:
         return _bernoulli_pass_py(partition_sizes, fraction, seed)
     bases = np.concatenate([[0], np.cumsum(partition_sizes)[:-1]]).astype(np.int64)
     world = comm.world if comm is not None else 1
     rank = comm.rank if comm is not None else 0
     mine = [p for p in range(len(partition_sizes)) if p % world == rank and partition_sizes[p] > 0]
-    if len(mine) > 1:
+    parts = None
+    if device is not None and mine:
+        picks = device(np.array([seed ^ p for p in mine], dtype=np.uint64),
+                       np.array([partition_sizes[p] for p in mine], dtype=np.int64), bases[mine], fraction)
+        parts = None if picks is None else [picks]
+    if parts is None and len(mine) > 1:
         from concurrent.futures import ThreadPoolExecutor
         with ThreadPoolExecutor(max_workers=min(len(mine), 16)) as ex:
             parts = list(ex.map(lambda p: _partition_picks(p, int(bases[p]), int(partition_sizes[p]), fraction,
                                                            seed), mine))
-    else:
+    elif parts is None:
         parts = [_partition_picks(p, int(bases[p]), int(partition_sizes[p]), fraction, seed) for p in mine]
     local = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int64)
     if world > 1:
@@ -125,9 +133,11 @@ def _bernoulli_pass(partition_sizes: Sequence[int], fraction: float, seed: int, 
     return np.sort(local, kind="stable").tolist()
 
 
-def take_sample(partition_sizes: Sequence[int], num: int, seed: Optional[int], comm=None) -> List[int]:
+def take_sample(partition_sizes: Sequence[int], num: int, seed: Optional[int], comm=None,
+                device=None) -> List[int]:
     """Global row indices that ``takeSample(False, num, seed)`` returns, in order.
-    With ``comm`` every rank must call it with the same arguments."""
+    With ``comm`` every rank must call it with the same arguments; ``device``
+    runs the Bernoulli passes on the GPU (see ``_bernoulli_pass``)."""
     if num < 0:
         raise ValueError("Sample size cannot be negative.")
     total = int(sum(partition_sizes))
@@ -143,9 +153,9 @@ def take_sample(partition_sizes: Sequence[int], num: int, seed: Optional[int], c
         rand.shuffle(idx)
         return idx
     fraction = _fraction(num, total)
-    samples = _bernoulli_pass(partition_sizes, fraction, seed, comm)
+    samples = _bernoulli_pass(partition_sizes, fraction, seed, comm, device)
     while len(samples) < num:
         seed = rand.randint(0, sys.maxsize)
-        samples = _bernoulli_pass(partition_sizes, fraction, seed, comm)
+        samples = _bernoulli_pass(partition_sizes, fraction, seed, comm, device)
     rand.shuffle(samples)
     return samples[0:num]

@@ -135,6 +135,19 @@ int km_commit(km_ctx* ctx);
  * (kmeans_spark.py:72, 196). */
 int km_gather_rows(km_ctx* ctx, const int64_t* local_idx, int32_t n, double* out);
 
+/* Bernoulli pass of rdd.takeSample(False, num, seed) (kmeans_spark.py:72,
+ * 196; PySpark RDD.takeSample + RDDSampler): for each of the nparts given
+ * partitions, row i is kept when the i-th double of Python's
+ * random.Random(seeds[p]) (seeds[p] = takeSample seed ^ partition index,
+ * after ten randint(0, 1) warm-up draws) is < fraction.  One wave per
+ * partition on this context's GPU.  out[0..*n_out): global row indices
+ * bases[p] + i, partitions in the given order, rows ascending.  KM_ERR_ARG
+ * when a partition yields more picks than the device pass holds (4x the
+ * expectation + 64) or *n_out would exceed cap: the caller then samples on
+ * the host. */
+int km_bernoulli_sample(km_ctx* ctx, const uint64_t* seeds, const int64_t* sizes, const int64_t* bases,
+                        int32_t nparts, double fraction, int64_t* out, int64_t cap, int64_t* n_out);
+
 /* Labels of every local row for the current centroids: replaces predict's
  * assign_partition (kmeans_spark.py:343-350). */
 int km_predict(km_ctx* ctx, int32_t* labels_out);
