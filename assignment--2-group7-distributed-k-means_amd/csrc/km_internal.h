@@ -13,7 +13,7 @@ struct QEntry {
   uint32_t row;   // local row
   uint32_t i1;    // best screened centroid
   uint32_t i2;    // second best screened centroid
-  uint32_t kind;  // 1 = re-rank {i1,i2}, 2 = full exact scan
+  uint32_t kind;  // 1 = re-rank {i1,i2}, 2 = full exact scan, 3 = scan of the chain j & 7 == i1 & 7
 };
 
 // Per-iteration status produced on device by k_finalize (kmeans_spark.py:176-313

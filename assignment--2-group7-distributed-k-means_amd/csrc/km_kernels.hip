@@ -1101,6 +1101,22 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
     const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k3));
     uint32_t kind = 0;
     if (!(k2 - k1 > thr2)) kind = (same_chain || !(k3 - k1 > thr3)) ? 2u : 1u;
+    // p1, p2 in one chain but every other chain's best separated from k1: the
+    // answer lies in that chain (j & 7 == p1 & 7), scanned exactly (kind 3,
+    // k/8 centroids) instead of all k.  Rare: behind a wave-uniform branch.
+    if (__ballot(kind == 2u && same_chain) != 0ull) {
+      const uint32_t cs = p1 & 7u;
+      float o = FLT_MAX;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t v0, v1;  // chain c of lane half 0 (id c) and of half 1 (id 4 + c)
+        perm_halves(__float_as_uint(a1[c]), v0, v1);
+        if ((uint32_t)c != cs) o = kmin(o, __uint_as_float(v0));
+        if ((uint32_t)(4 + c) != cs) o = kmin(o, __uint_as_float(v1));
+      }
+      const float thr3x = 2.0f * B0 + rho * (fabsf(k1) + fabsf(o));
+      if (kind == 2u && same_chain && o - k1 > thr3x) kind = 3u;
+    }
     if constexpr (ABL == 7) {
       __builtin_amdgcn_sched_barrier(0);
       const unsigned long long tnow = __builtin_amdgcn_s_memtime();
@@ -1113,6 +1129,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
     const bool enq = (h == 0) && valid && (kind != 0);
     const uint64_t m = __ballot(enq);
     if (m) {
+      // re-rank entries from the front, full and chain scans from the back
       const uint64_t m1 = __ballot(enq && kind == 1);
       const uint64_t m2 = m & ~m1;
       const uint64_t below = (1ull << lane) - 1ull;
@@ -1463,8 +1480,8 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
       q = queue[(size_t)sg * ql.seg + (g - pre[sg])];
     }
     const bool ok = have && q.i1 < (uint32_t)k && q.i2 < (uint32_t)k;
-    const int a = ok ? (int)min(q.i1, q.i2) : 0, bb = ok ? (int)max(q.i1, q.i2) : 0;
     const float* __restrict__ x = X + (size_t)q.row * dp;
+    const int a = ok ? (int)min(q.i1, q.i2) : 0, bb = ok ? (int)max(q.i1, q.i2) : 0;
     const double* __restrict__ ca = C64 + (size_t)a * d;
     const double* __restrict__ cb = C64 + (size_t)bb * d;
     double sa, sb;
@@ -1474,8 +1491,8 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
                 tb = np_sq(cb[f], xf);
               },
               0, d, u, sa, sb);
-    if (!have) continue;
     int lab = np_pick_second(sqrt(sa), sqrt(sb)) ? bb : a;
+    if (!have) continue;
     if (!ok && u == 0) {
       // corrupt candidate (cannot happen for finite data): full scan
       double best = 0.0;
@@ -1543,18 +1560,69 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
   for (uint32_t b0 = blockIdx.x * per_batch; b0 < total; b0 += gridDim.x * per_batch) {
     uint32_t rows[G];
     bool have[G];
+    int chain[G];  // kind 3: the chain j & 7 to scan, else -1
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const uint32_t e = b0 + (uint32_t)(wave * G + g);
       have[g] = e < total;
       rows[g] = 0;
+      chain[g] = -1;
       if (have[g]) {
         const uint32_t sg = find_segment(pre, ql.nwaves, e);
         const QEntry* qp = queue + (size_t)sg * ql.seg + (ql.seg - 1u - (e - pre[sg]));
         rows[g] = __builtin_amdgcn_readfirstlane(qp->row);
+        const uint32_t kind = __builtin_amdgcn_readfirstlane(qp->kind);
+        const uint32_t i1 = __builtin_amdgcn_readfirstlane(qp->i1);
+        if (kind == 3u && i1 < (uint32_t)k) chain[g] = (int)(i1 & 7u);
         const float* x = X + (size_t)rows[g] * dp;
         for (int f = lane; f < d; f += 64) xs[g * d + f] = x[f];
       }
+    }
+    // np.argmin across lanes (first NaN, else smallest value, lowest index),
+    // then the label and, when fused, the point's row into the sums
+    auto finish = [&](int g, double bv, int bi) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const double ob = __shfl_xor(bv, o);
+        const int oj = __shfl_xor(bi, o);
+        bool take = false;
+        if (oj >= 0) {
+          if (bi < 0) {
+            take = true;
+          } else {
+            const bool on = ob != ob, mn = bv != bv;
+            take = (on && !mn) || (on == mn && (on ? oj < bi : (ob < bv || (ob == bv && oj < bi))));
+          }
+        }
+        if (take) {
+          bv = ob;
+          bi = oj;
+        }
+      }
+      const int lab = bi < 0 ? 0 : bi;
+      if (lane == 0) labels[rows[g]] = lab;
+      if (stats) {
+        for (int f = lane; f < d; f += 64) atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)xs[g * d + f]);
+        if (lane == 0) atomicAdd(stats + (size_t)lab * (d + 1) + d, 1.0);  // count
+      }
+    };
+    // chain scans (kind 3): the wave evaluates members j = chain + 8 m, lanes
+    // over m, straight from C64T (no barriers: done before the chunk loop)
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (!have[g] || chain[g] < 0) continue;
+      double bv = 0.0;
+      int bi = -1;
+      for (int j = chain[g] + 8 * lane; j < k; j += 8 * 64) {
+        const float* xg = xs + g * d;
+        const double v = np_norm([&](int f) { return np_sq(C64T[(size_t)f * k + j], xg[f]); }, d);
+        if (np_better(v, bv, bi >= 0)) {
+          bv = v;
+          bi = j;
+        }
+      }
+      finish(g, bv, bi);
+      have[g] = false;
     }
     double best[G];
     int bj[G];
@@ -1587,36 +1655,8 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
       }
     }
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      if (!have[g]) continue;
-      double bv = best[g];
-      int bi = bj[g];
-      // np.argmin across lanes: first NaN, else smallest value, lowest index
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) {
-        const double ob = __shfl_xor(bv, o);
-        const int oj = __shfl_xor(bi, o);
-        bool take = false;
-        if (oj >= 0) {
-          if (bi < 0) {
-            take = true;
-          } else {
-            const bool on = ob != ob, mn = bv != bv;
-            take = (on && !mn) || (on == mn && (on ? oj < bi : (ob < bv || (ob == bv && oj < bi))));
-          }
-        }
-        if (take) {
-          bv = ob;
-          bi = oj;
-        }
-      }
-      const int lab = bi < 0 ? 0 : bi;
-      if (lane == 0) labels[rows[g]] = lab;
-      if (stats) {
-        for (int f = lane; f < d; f += 64) atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)xs[g * d + f]);
-        if (lane == 0) atomicAdd(stats + (size_t)lab * (d + 1) + d, 1.0);  // count
-      }
-    }
+    for (int g = 0; g < G; ++g)
+      if (have[g]) finish(g, best[g], bj[g]);
   }
 }
 
