@@ -547,6 +547,16 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
         top3_insert(a1[reg & 3], a2[reg & 3], a3[reg & 3], key);
       }
     };
+    // top-2 chains: registers ra = 8 (pp >> 2) + (pp & 3) and ra + 4 (one
+    // chain) folded in together, 5 VALU per 2 keys (as in k_fused)
+    auto key_pair = [&](const f32x16& acc, int pp) {
+      const int c = pp & 3, ra = 8 * (pp >> 2) + c, rb = ra + 4;
+      const float ka = __uint_as_float((__float_as_uint(acc[ra]) & ~maskq) | jg[ra >> 2]);
+      const float kb = __uint_as_float((__float_as_uint(acc[rb]) & ~maskq) | jg[rb >> 2]);
+      const float tm = __builtin_amdgcn_fmed3f(a1[c], ka, kb);
+      a1[c] = __builtin_fminf(__builtin_fminf(a1[c], ka), kb);
+      a2[c] = __builtin_fminf(a2[c], tm);
+    };
     // MFMAs of block `blk` into `cur` while the 16 key updates of the
     // previous block (`prev`, index words already in jg) fill the gaps.  A
     // fragments are prefetched one K-step ahead (into the next block at the
@@ -558,9 +568,15 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
       for (int t = 0; t < NS; ++t) {
         const Frag nx = (t + 1 < NS) ? load_frag(blk, t + 1) : load_frag(blk + 1 < nblk ? blk + 1 : blk, 0);
         cur = mfma3(cur, fr, t);
+        if constexpr (T2 && ABL != 1) {
 #pragma unroll
-        for (int rr = 0; rr < 16; ++rr)
-          if (rr * NS / 16 == t) key_update(prev, rr);
+          for (int pp = 0; pp < 8; ++pp)
+            if (pp * NS / 8 == t) key_pair(prev, pp);
+        } else {
+#pragma unroll
+          for (int rr = 0; rr < 16; ++rr)
+            if (rr * NS / 16 == t) key_update(prev, rr);
+        }
         fr = nx;
       }
     };
@@ -591,8 +607,13 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
       set_jg(jq0 + 8u * (uint32_t)(blk - 1));
       overlapped(accB, blk, nb, accA);
       set_jg(jq0 + 8u * (uint32_t)blk);
+      if constexpr (T2 && ABL != 1) {
 #pragma unroll
-      for (int rr = 0; rr < 16; ++rr) key_update(accB, rr);
+        for (int pp = 0; pp < 8; ++pp) key_pair(accB, pp);
+      } else {
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) key_update(accB, rr);
+      }
     }
     if (nchunks > 1 && tile >= ntiles) continue;
 
@@ -994,7 +1015,8 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       return acc;
     };
     // register reg holds centroid j = 32 blk + 4h + (reg & 3) + 8 (reg >> 2);
-    // chain reg & 3 keeps the top two keys (score | j >> 2)
+    // chain reg & 3 keeps the top two keys (score | j >> 2); registers reg and
+    // reg + 4 (same chain) are folded in together
     auto keys_block = [&](const f32x16& acc, int blk) {
       if constexpr (ABL == 1 || ABL == 5 || ABL == 6) {
         a1[blk & 3] = fminf(a1[blk & 3], acc[0] + acc[15]);
@@ -1002,14 +1024,20 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
         return;
       }
       const uint32_t jq = (uint32_t)(8 * blk + h);
+      // two keys of one chain per step: new best = min3(best, ka, kb), new
+      // second = min(second, med3(best, ka, kb)) -- the same top two as one
+      // key at a time, 5 VALU per 2 scores instead of 6 (c3: -2% kernel time)
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const float key = __uint_as_float((__float_as_uint(acc[reg]) & ~maskq) | (jq | (uint32_t)(2 * (reg >> 2))));
-        const int c = reg & 3;
-        const float n1 = __builtin_amdgcn_fmed3f(a1[c], key, -FLT_MAX);
-        a2[c] = __builtin_amdgcn_fmed3f(a1[c], a2[c], key);
-        a1[c] = n1;
-      }
+      for (int q = 0; q < 16; q += 8)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int ra = q + c, rb = q + c + 4;
+          const float ka = __uint_as_float((__float_as_uint(acc[ra]) & ~maskq) | (jq | (uint32_t)(2 * (ra >> 2))));
+          const float kb = __uint_as_float((__float_as_uint(acc[rb]) & ~maskq) | (jq | (uint32_t)(2 * (rb >> 2))));
+          const float t = __builtin_amdgcn_fmed3f(a1[c], ka, kb);
+          a1[c] = __builtin_fminf(__builtin_fminf(a1[c], ka), kb);
+          a2[c] = __builtin_fminf(a2[c], t);
+        }
     };
     // software pipeline: block blk's MFMAs overlap block blk-1's key
     // updates (started two MFMAs in, once blk-1's scores have landed); the
