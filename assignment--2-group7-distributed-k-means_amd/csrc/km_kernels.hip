@@ -926,6 +926,14 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       Ahi[b][t] = __builtin_bit_cast(f16x8, A.ChiF[(b * NS + t) * 64 + lane]);
       Alo[b][t] = __builtin_bit_cast(f16x8, A.CloF[(b * NS + t) * 64 + lane]);
     }
+  // consume the image loads here: otherwise the loop's AGPR touches inherit
+  // them as outstanding and the waitcnt pass drains vmcnt to 0 in every loop
+  // iteration -- including the next tile's prefetch (one exposed HBM round
+  // trip per two tiles)
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int t = 0; t < NS; ++t) asm volatile("" : "+a"(Ahi[b][t]), "+a"(Alo[b][t]));
   __syncthreads();
 
   const float s = mfma_scale(*A.xabs, *A.cabs);
@@ -1205,15 +1213,18 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
 
   // tiles of this wave, two register buffers: the next tile's rows are in
   // flight while this one is processed
+  // (loads are unconditional -- load_tile clamps past-the-end rows to row
+  // n - 1 -- so every path reaching a wait has the same loads in flight and
+  // the waitcnt pass can wait for the current tile only, not vmcnt(0))
   float4 xb0[NS][2], xb1[NS][2];
   float xn0 = 0.0f, xn1 = 0.0f;
-  if ((int64_t)gw < ntiles) load_tile(gw, xb0, xn0);
+  load_tile(gw, xb0, xn0);
   for (int64_t tile = gw; tile < ntiles; tile += 2 * tstride) {
     const int64_t t1 = tile + tstride;
-    if (t1 < ntiles) load_tile(t1, xb1, xn1);
+    load_tile(t1, xb1, xn1);
     process_tile(tile, xb0, xn0);
     if (t1 >= ntiles) break;
-    if (t1 + tstride < ntiles) load_tile(t1 + tstride, xb0, xn0);
+    load_tile(t1 + tstride, xb0, xn0);
     process_tile(t1, xb1, xn1);
   }
   if (lane == 0) {
