@@ -331,6 +331,7 @@ hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C
 static constexpr int MFMA_LDS_LARGE = 160 * 1024;  // LDS per CU
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
 // power-of-two scale: max(|x|, |c|) * s < 2^14 (so |-2cs| < 2^15 < 65504);
 // 1 for non-finite or all-zero data (the keys then force the exact path)
@@ -972,12 +973,24 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
     for (int t = 0; t < NS; ++t) {
       const float xv[8] = {xc[t][0].x, xc[t][0].y, xc[t][0].z, xc[t][0].w,
                            xc[t][1].x, xc[t][1].y, xc[t][1].z, xc[t][1].w};
+      // hi = RN_f16(xs) (v_cvt_pk_f16_f32), lo = RN_f16(xs - hi) with one
+      // v_fma_mix per element (the compiler's own choice is cvt back to f32,
+      // v_pk_fma, cvt_pk: 2 VALU per element instead of 1; same bits,
+      // scripts/probes/split_mix.hip)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float xs = xv[e] * s;
-        const _Float16 hi = (_Float16)xs;
-        bh[t][e] = hi;
-        bl[t][e] = (_Float16)__builtin_fmaf((float)hi, -1.0f, xs);  // v_fma_mix{lo,hi}_f16
+      for (int e = 0; e < 8; e += 2) {
+        const float xs0 = xv[e] * s, xs1 = xv[e + 1] * s;
+        const f16x2 hp = {(_Float16)xs0, (_Float16)xs1};
+        uint32_t lp;
+        asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
+            "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+            : "=&v"(lp)
+            : "v"(__builtin_bit_cast(uint32_t, hp)), "v"(xs0), "v"(xs1));
+        const f16x2 lo = __builtin_bit_cast(f16x2, lp);
+        bh[t][e] = hp[0];
+        bh[t][e + 1] = hp[1];
+        bl[t][e] = lo[0];
+        bl[t][e + 1] = lo[1];
       }
     }
     if constexpr (ABL == 7) {
@@ -1585,7 +1598,7 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
                                                    const double* __restrict__ C64T, const QEntry* __restrict__ queue,
                                                    const uint32_t* __restrict__ qcount, QLayout ql,
                                                    int32_t* __restrict__ labels, int ch,
-                                                   double* __restrict__ stats) {
+                                                   double* __restrict__ stats, int use_chain) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sCT = reinterpret_cast<double*>(smem);                                    // [d][ch]
   float* xs_all = reinterpret_cast<float*>(smem + (size_t)d * ch * 8);              // [8][G][d]
@@ -1600,23 +1613,33 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
     uint32_t rows[G];
     bool have[G];
     int chain[G];  // kind 3: the chain j & 7 to scan, else -1
+    // the G entries' queue words, then their rows, each as one batch of
+    // independent loads (past-the-end slots read the last entry, unused)
+    QEntry qe[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const uint32_t e = b0 + (uint32_t)(wave * G + g);
       have[g] = e < total;
-      rows[g] = 0;
-      chain[g] = -1;
-      if (have[g]) {
-        const uint32_t sg = find_segment(pre, ql.nwaves, e);
-        const QEntry* qp = queue + (size_t)sg * ql.seg + (ql.seg - 1u - (e - pre[sg]));
-        rows[g] = __builtin_amdgcn_readfirstlane(qp->row);
-        const uint32_t kind = __builtin_amdgcn_readfirstlane(qp->kind);
-        const uint32_t i1 = __builtin_amdgcn_readfirstlane(qp->i1);
-        if (kind == 3u && i1 < (uint32_t)k) chain[g] = (int)(i1 & 7u);
-        const float* x = X + (size_t)rows[g] * dp;
-        for (int f = lane; f < d; f += 64) xs[g * d + f] = x[f];
-      }
+      const uint32_t ec = have[g] ? e : total - 1u;
+      const uint32_t sg = find_segment(pre, ql.nwaves, ec);
+      qe[g] = queue[(size_t)sg * ql.seg + (ql.seg - 1u - (ec - pre[sg]))];
     }
+    float xv[G][4];  // d <= 256
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      rows[g] = __builtin_amdgcn_readfirstlane(qe[g].row);
+      const uint32_t kind = __builtin_amdgcn_readfirstlane(qe[g].kind);
+      const uint32_t i1 = __builtin_amdgcn_readfirstlane(qe[g].i1);
+      chain[g] = (use_chain && have[g] && kind == 3u && i1 < (uint32_t)k) ? (int)(i1 & 7u) : -1;
+      const float* x = X + (size_t)rows[g] * dp;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xv[g][u] = (lane + 64 * u < d) ? x[lane + 64 * u] : 0.0f;
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (lane + 64 * u < d) xs[g * d + lane + 64 * u] = xv[g][u];
     // np.argmin across lanes (first NaN, else smallest value, lowest index),
     // then the label and, when fused, the point's row into the sums
     auto finish = [&](int g, double bv, int bi) {
@@ -1717,8 +1740,9 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   const int ch = g.d <= 128 ? 64 : 32;  // chunk columns: <= 64 KiB of LDS
   const size_t fs_lds = (size_t)g.d * ch * 8 + (size_t)8 * G * g.d * 4 + pre_bytes;
   if (fs_lds > LDS_MAX) return hipErrorInvalidValue;
+  static const int use_chain = small_env("KM_CHAIN", 1);
   hipLaunchKernelGGL(k_fullscan<G>, dim3(n_cu), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T, queue, qcount, ql,
-                     labels, ch, stats);
+                     labels, ch, stats, use_chain);
   return hipGetLastError();
 }
 
