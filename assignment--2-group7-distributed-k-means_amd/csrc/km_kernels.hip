@@ -1516,9 +1516,11 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* tab = reinterpret_cast<double*>(smem);
   uint32_t* pre = reinterpret_cast<uint32_t*>(smem + (stats && tab_kp ? (size_t)(d + 1) * tab_kp * 8 : 0));
+  uint32_t* pre1 = pre + ql.nwaves + 1;  // full / chain scan entries (their sums only)
   if (stats && tab_kp)
     for (int i = threadIdx.x; i < (d + 1) * tab_kp; i += blockDim.x) tab[i] = 0.0;
   block_prefix(qcount, 0, ql.nwaves, pre);
+  if (stats) block_prefix(qcount, 1, ql.nwaves, pre1);
   const uint32_t total = pre[ql.nwaves];
   const int u = threadIdx.x & 7;
   const uint32_t ng = (gridDim.x * blockDim.x) >> 3;
@@ -1567,6 +1569,32 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
           atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)x[f]);
       }
       if (u == 0) {  // count
+        if (tab_kp)
+          atomicAdd(tab + (size_t)d * tab_kp + lab, 1.0);
+        else
+          atomicAdd(stats + (size_t)lab * (d + 1) + d, 1.0);
+      }
+    }
+  }
+  if (stats) {
+    // rows of the entries k_fullscan resolved (launched first: their labels
+    // are final) into the same table -- one global float64 atomic per table
+    // entry instead of one per feature per point, which serialised on the
+    // few clusters that collect most scanned points (c3 k_fullscan 0.42 -> 0.38 ms)
+    const uint32_t total1 = pre1[ql.nwaves];
+    const uint32_t g0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+    for (uint32_t g = g0; g < total1; g += ng) {
+      const uint32_t sg = find_segment(pre1, ql.nwaves, g);
+      const QEntry q = queue[(size_t)sg * ql.seg + (ql.seg - 1u - (g - pre1[sg]))];
+      const int lab = labels[q.row];
+      const float* __restrict__ x = X + (size_t)q.row * dp;
+      for (int f = u; f < d; f += 8) {
+        if (tab_kp)
+          atomicAdd(tab + (size_t)f * tab_kp + lab, (double)x[f]);
+        else
+          atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)x[f]);
+      }
+      if (u == 0) {
         if (tab_kp)
           atomicAdd(tab + (size_t)d * tab_kp + lab, 1.0);
         else
@@ -1688,11 +1716,16 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
     }
     double best[G];
     int bj[G];
+    bool any_full = false;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       best[g] = 0.0;
       bj[g] = -1;
+      any_full |= have[g];
     }
+    // most batches hold chain scans only: skip the chunk pass unless some
+    // wave of the workgroup still has a full scan
+    if (!__syncthreads_or(any_full)) continue;
     for (int c0 = 0; c0 < k; c0 += ch) {
       __syncthreads();  // the previous chunk is consumed (and the rows staged)
       const int cw = min(ch, k - c0);
@@ -1728,21 +1761,25 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   if (g.n == 0 || ql.nwaves == 0) return hipSuccess;
   constexpr size_t LDS_MAX = 160 * 1024;
   const size_t pre_bytes = ((size_t)ql.nwaves + 1) * 4;
-  if (pre_bytes > LDS_MAX / 2) return hipErrorInvalidValue;
-  const size_t tab_bytes = (size_t)(g.d + 1) * g.kp * 8;
-  const int tab_kp = (stats && tab_bytes + pre_bytes <= LDS_MAX) ? g.kp : 0;
-  hipLaunchKernelGGL(k_rerank2, dim3(n_cu), dim3(1024), (tab_kp ? tab_bytes : 0) + pre_bytes, s, X, g.dp, g.d, g.k,
-                     C64, queue, qcount, ql, labels, stats, tab_kp);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (pre_bytes > LDS_MAX / 4) return hipErrorInvalidValue;
   if (g.d > 256) return hipErrorInvalidValue;
+  // full / chain scans first (labels only); k_rerank2 then adds the sums of
+  // both queues through its LDS table
   constexpr int G = 4;
   const int ch = g.d <= 128 ? 64 : 32;  // chunk columns: <= 64 KiB of LDS
   const size_t fs_lds = (size_t)g.d * ch * 8 + (size_t)8 * G * g.d * 4 + pre_bytes;
   if (fs_lds > LDS_MAX) return hipErrorInvalidValue;
   static const int use_chain = small_env("KM_CHAIN", 1);
-  hipLaunchKernelGGL(k_fullscan<G>, dim3(n_cu), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T, queue, qcount, ql,
-                     labels, ch, stats, use_chain);
+  static const int fs_wg = small_env("KM_FS_WG", 1);  // workgroups per CU (3: no measurable change)
+  hipLaunchKernelGGL(k_fullscan<G>, dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T, queue, qcount,
+                     ql, labels, ch, (double*)nullptr, use_chain);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t tab_bytes = (size_t)(g.d + 1) * g.kp * 8;
+  const size_t pres = (stats ? 2 : 1) * pre_bytes;
+  const int tab_kp = (stats && tab_bytes + pres <= LDS_MAX) ? g.kp : 0;
+  hipLaunchKernelGGL(k_rerank2, dim3(n_cu), dim3(1024), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d, g.k,
+                     C64, queue, qcount, ql, labels, stats, tab_kp);
   return hipGetLastError();
 }
 
