@@ -1626,7 +1626,7 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
                                                    const double* __restrict__ C64T, const QEntry* __restrict__ queue,
                                                    const uint32_t* __restrict__ qcount, QLayout ql,
                                                    int32_t* __restrict__ labels, int ch,
-                                                   double* __restrict__ stats, int use_chain) {
+                                                   double* __restrict__ stats, int use_chain, int pair_chain) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sCT = reinterpret_cast<double*>(smem);                                    // [d][ch]
   float* xs_all = reinterpret_cast<float*>(smem + (size_t)d * ch * 8);              // [8][G][d]
@@ -1698,6 +1698,34 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
     };
     // chain scans (kind 3): the wave evaluates members j = chain + 8 m, lanes
     // over m, straight from C64T (no barriers: done before the chunk loop)
+    // k <= 256: a chain has <= 32 members, so two entries share a pass (lane
+    // half e of the wave on entry p + e); the other half enters the 64-lane
+    // argmin with no candidate
+    if (k <= 256 && pair_chain) {
+      static_assert(G % 2 == 0, "entry pairs");
+#pragma unroll
+      for (int p = 0; p < G; p += 2) {
+        const bool a0 = have[p] && chain[p] >= 0, a1 = have[p + 1] && chain[p + 1] >= 0;
+        if (!a0 && !a1) continue;
+        const int e = lane >> 5;
+        const int j = (e ? chain[p + 1] : chain[p]) + 8 * (lane & 31);
+        double bv = 0.0;
+        int bi = -1;
+        if ((e ? a1 : a0) && j < k) {
+          const float* xg = xs + (p + e) * d;
+          bv = np_norm([&](int f) { return np_sq(C64T[(size_t)f * k + j], xg[f]); }, d);
+          bi = j;
+        }
+        if (a0) {
+          finish(p, e == 0 ? bv : 0.0, e == 0 ? bi : -1);
+          have[p] = false;
+        }
+        if (a1) {
+          finish(p + 1, e == 1 ? bv : 0.0, e == 1 ? bi : -1);
+          have[p + 1] = false;
+        }
+      }
+    }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       if (!have[g] || chain[g] < 0) continue;
@@ -1765,14 +1793,20 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   if (g.d > 256) return hipErrorInvalidValue;
   // full / chain scans first (labels only); k_rerank2 then adds the sums of
   // both queues through its LDS table
-  constexpr int G = 4;
+  static const int fs_g = small_env("KM_FS_G", 2);  // entries per wave: 2 or 4
+  const int G = fs_g == 4 ? 4 : 2;
   const int ch = g.d <= 128 ? 64 : 32;  // chunk columns: <= 64 KiB of LDS
   const size_t fs_lds = (size_t)g.d * ch * 8 + (size_t)8 * G * g.d * 4 + pre_bytes;
   if (fs_lds > LDS_MAX) return hipErrorInvalidValue;
   static const int use_chain = small_env("KM_CHAIN", 1);
+  static const int pair_chain = small_env("KM_PAIR_CHAIN", 1);
   static const int fs_wg = small_env("KM_FS_WG", 1);  // workgroups per CU (3: no measurable change)
-  hipLaunchKernelGGL(k_fullscan<G>, dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T, queue, qcount,
-                     ql, labels, ch, (double*)nullptr, use_chain);
+  if (G == 4)
+    hipLaunchKernelGGL(k_fullscan<4>, dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T, queue,
+                       qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain);
+  else
+    hipLaunchKernelGGL(k_fullscan<2>, dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T, queue,
+                       qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t tab_bytes = (size_t)(g.d + 1) * g.kp * 8;
