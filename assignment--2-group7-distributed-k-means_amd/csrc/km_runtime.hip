@@ -114,7 +114,8 @@ struct km_ctx {
   float* pinned = nullptr;
   size_t pinned_floats = 0;
   // profiling
-  bool prof = false;
+  int prof = 0;                  // bitmask of KM_K_* phases timed with events
+  const double* prep_of = nullptr;  // the centroid buffer the derived images were built from
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[KM_K_COUNT];
   std::vector<hipEvent_t> pool;
 
@@ -137,14 +138,14 @@ struct ProfScope {
   int kind;
   hipEvent_t a = nullptr, b = nullptr;
   ProfScope(km_ctx* ctx, int k) : c(ctx), kind(k) {
-    if (c->prof) {
+    if ((c->prof >> kind) & 1) {
       a = c->take_event();
       b = c->take_event();
       (void)hipEventRecord(a, c->stream);
     }
   }
   ~ProfScope() {
-    if (c->prof) {
+    if ((c->prof >> kind) & 1) {
       (void)hipEventRecord(b, c->stream);
       c->ev[kind].emplace_back(a, b);
     }
@@ -197,9 +198,13 @@ void free_data(km_ctx* c) {
   c->loaded = false;
 }
 
-int prep(km_ctx* c) {
+// derived images (fp32 copy, transposed f64, fp16 hi/lo split, norms, bound
+// constants) of centroid buffer `src` (C64_cur, or C64_new speculatively in
+// km_update so the next iteration's assign starts right after the host sync)
+int prep(km_ctx* c, const double* src) {
   ProfScope ps(c, KM_K_PREP);
-  KM_HIP(km::launch_prep_centroids(c->C64_cur, c->g, c->C32, c->cn2, c->cmax, c->cabs, c->C64T, c->stream));
+  c->prep_of = src;
+  KM_HIP(km::launch_prep_centroids(src, c->g, c->C32, c->cn2, c->cmax, c->cabs, c->C64T, c->stream));
   KM_HIP(km::launch_prep_split(c->C32, c->g, c->cn2, c->xabs, c->cabs, c->Chi, c->Clo, c->cn2s, c->stream));
   KM_HIP(km::launch_bound_consts(c->cmax, c->xabs, c->cabs, c->g.dp, c->bnd, c->stream));
   return KM_OK;
@@ -215,8 +220,14 @@ int ensure_scratch(km_ctx* c, int64_t rows) {
   return KM_OK;
 }
 
+int prep(km_ctx* c) { return prep(c, c->C64_cur); }
+
 int run_assign(km_ctx* c, bool with_stats) {
   const km::Geometry& g = c->g;
+  if (c->prep_of != c->C64_cur) {
+    const int rc = prep(c);
+    if (rc != KM_OK) return rc;
+  }
   c->ql = km::QLayout{0, 0};
   if (with_stats) KM_HIP(hipMemsetAsync(c->stats, 0, sizeof(double) * (size_t)g.k * (g.d + 1), c->stream));
   if (c->path == 1) {
@@ -551,6 +562,12 @@ int km_update(km_ctx* c, km_status* st, int64_t* counts) {
   }
   KM_HIP(hipMemcpyAsync(c->status_host, c->status_dev, sizeof(km::DevStatus), hipMemcpyDeviceToHost, c->stream));
   KM_HIP(hipMemcpyAsync(c->counts_host, c->counts_dev, sizeof(int64_t) * c->g.k, hipMemcpyDeviceToHost, c->stream));
+  {
+    // images of the new centroids for the next iteration, queued behind the
+    // status copies (used after km_commit unless km_replace_rows changes them)
+    const int rc = prep(c, c->C64_new);
+    if (rc != KM_OK) return rc;
+  }
   KM_HIP(hipStreamSynchronize(c->stream));
   const km::DevStatus& s = *c->status_host;
   if (st) {
@@ -569,6 +586,7 @@ int km_replace_rows(km_ctx* c, const int32_t* ids, const double* rows, int32_t n
   KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_replace_rows: set centroids first");
   KM_REQUIRE(n >= 0 && (n == 0 || (ids && rows)), KM_ERR_ARG, "km_replace_rows: bad args");
   KM_HIP(hipSetDevice(c->device));
+  if (n > 0 && c->prep_of == c->C64_new) c->prep_of = nullptr;  // its images are stale now
   for (int i = 0; i < n; ++i) {
     KM_REQUIRE(ids[i] >= 0 && ids[i] < c->g.k, KM_ERR_ARG, "km_replace_rows: cluster id out of range");
     KM_HIP(hipMemcpyAsync(c->C64_new + (size_t)ids[i] * c->g.d, rows + (size_t)i * c->g.d,
@@ -582,7 +600,7 @@ int km_commit(km_ctx* c) {
   KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_commit: set centroids first");
   KM_HIP(hipSetDevice(c->device));
   std::swap(c->C64_cur, c->C64_new);
-  return prep(c);
+  return c->prep_of == c->C64_cur ? KM_OK : prep(c);
 }
 
 int km_gather_rows(km_ctx* c, const int64_t* idx, int32_t n, double* out) {
@@ -676,7 +694,7 @@ int km_labels(km_ctx* c, int32_t* labels_out) {
 
 int km_profile(km_ctx* c, int32_t enable) {
   KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
-  c->prof = enable != 0;
+  c->prof = enable;  // bitmask of (1 << KM_K_*); -1 = every phase
   return KM_OK;
 }
 

@@ -190,8 +190,16 @@ class HipEngine:
         return {f: getattr(inf, f) for f, _ in inf._fields_}
 
     # -- profiling ---------------------------------------------------------------
-    def profile(self, enable: bool = True) -> None:
-        self._c(self.lib.km_profile(self.ctx, 1 if enable else 0), "km_profile")
+    _PHASES = {"assign": 0, "resolve": 1, "stats": 2, "update": 3, "prep": 4}   # KM_K_* (kmeans_amd.h)
+
+    def profile(self, enable: bool = True, phases=None) -> None:
+        """Time launches with HIP events: every phase, or only ``phases``
+        (names of ``_PHASES``).  Each event record costs a few microseconds of
+        stream time, so a timed region records only the phases it reports."""
+        mask = 0
+        if enable:
+            mask = -1 if phases is None else sum(1 << self._PHASES[p] for p in phases)
+        self._c(self.lib.km_profile(self.ctx, mask), "km_profile")
 
     def prof_read(self, kind: str) -> Tuple[float, int]:
         ms = ctypes.c_double()

@@ -154,7 +154,8 @@ int km_predict(km_ctx* ctx, int32_t* labels_out);
 /* Labels of the last km_assign_stats (device -> host). */
 int km_labels(km_ctx* ctx, int32_t* labels_out);
 
-/* Kernel timing with HIP events on the context stream. */
+/* Kernel timing with HIP events on the context stream.  `enable` is a
+ * bitmask of (1 << KM_K_*) phases to time (-1: all, 0: off). */
 int km_profile(km_ctx* ctx, int32_t enable);
 int km_prof_read(km_ctx* ctx, int32_t kind, double* total_ms, int64_t* launches);
 
