@@ -827,10 +827,10 @@ hipError_t launch_absmax(const float* X, int64_t nfloats, float* out, hipStream_
 // ---------------------------------------------------------------------------
 // Fused assign + partial statistics (c3 class: kp*dp <= 16384).
 //
-// One workgroup of 8 waves per CU (2 per SIMD).  The fp16 hi image of
-// -2*c*s lives in VGPRs (A fragments, NB*NS*4 registers per lane), the lo
-// image in LDS (NB*NS KiB, fragment-linear), and the rest of LDS holds this
-// workgroup's float64 partial sums, transposed [f][j] so that the 32 lanes
+// One workgroup of 4 waves per CU (1 per SIMD).  The fp16 hi and lo images
+// of -2*c*s live in AGPRs (A fragments, 2*NB*NS*4 registers per lane, read
+// by the MFMAs directly), LDS holds ||c||^2 s^2 and this workgroup's
+// float64 partial sums, transposed [f][j] so that the 32 lanes
 // of one ds_add_f64 (32 points, one feature) hit banks j mod 32.  Each wave
 // walks 32-point tiles: fp16x3 MFMA scores, four chains of top-2 keys
 // (score | j>>2), merged to the top-3 values and the best two indices, the
