@@ -34,5 +34,5 @@ ms_pred, n_pred = eng.prof_read("assign")
 eng.profile(False)
 ms_fit, ms_pred = ms_fit / max(n_fit, 1), ms_pred / max(n_pred, 1)  # prof_read: total ms, launches
 gb = N * d * 4 / 1e9
-print(f"{cfg}: assign+stats {ms_fit * 1e3:.1f} us ({gb / ms_fit:.0f} GB/s, {n_fit} launches); "
-      f"assign only {ms_pred * 1e3:.1f} us ({gb / ms_pred:.0f} GB/s, {n_pred} launches)")
+print(f"{cfg}: assign+stats {ms_fit * 1e3:.1f} us ({gb / ms_fit * 1e3:.0f} GB/s, {n_fit} launches); "
+      f"assign only {ms_pred * 1e3:.1f} us ({gb / ms_pred * 1e3:.0f} GB/s, {n_pred} launches)")
