@@ -1,0 +1,69 @@
+"""GPU parity at BASELINE.json's full single-GPU sizes, through properties that
+do not need the oracle to process every row:
+
+* counts: the per-cluster counts of the statistics pass sum to N and equal the
+  histogram of the labels it wrote;
+* checksum of checksums: sum_j n_j * c'_j (new centroids times counts, i.e. the
+  reduceByKey sums of kmeans_spark.py:169-188) equals sum_i x_i from an
+  independent float64 reduction of X;
+* cross-path idempotence: predict (the assign kernel without statistics,
+  kmeans_spark.py:343-350) returns exactly the labels of the fused
+  assign + statistics pass for the same centroids;
+* sampled labels: a seeded sample of rows, labelled by the oracle's restatement
+  of np.argmin(np.linalg.norm(C - x, axis=1)) (kmeans_spark.py:153-156),
+  bit-identical.
+
+c3 = N=100M, d=64, k=256 (the bench workload); c5 = N=50M, d=128, k=4096
+(one GPU holding all of it; the unfused MFMA path, chunked centroids, label-sort
+statistics); c4 = N=1B, d=32, k=1024 (128 GB resident on one GPU: 64-bit row
+indexing, statistics tiled over feature ranges).
+"""
+import numpy as np
+import pytest
+
+from oracle import kmeans_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("N,d,k,centers,sample,chunk", [
+    (100_000_000, 64, 256, 256, 20000, 1024),      # c3
+    (50_000_000, 128, 4096, 4096, 3000, 48),       # c5
+    (1_000_000_000, 32, 1024, 1024, 3000, 256),    # c4: 128 GB of rows on one GPU
+])
+def test_full_size_properties(N, d, k, centers, sample, chunk):
+    import kmeans_amd
+    from kmeans_amd.comm import Communicator
+
+    km = kmeans_amd.KMeans(k=k, max_iter=1, tolerance=1e-12, seed=42, compute_sse=True)
+    km.verbose = False
+    data = kmeans_amd.DeviceBlobs(n=N, d=d, n_centers=centers, box=10.0, std=1.0, seed=2024)
+    run = km._make_runner(data, Communicator())
+    eng = run.engine
+    C0 = km._initialize_centroids(run)
+    eng.set_centroids(C0)
+    sx = eng.sum_x()
+
+    eng.assign_stats()
+    st, counts = eng.update()
+    C1 = eng.get_centroids(1)
+    labels = eng.labels()
+    assert labels.shape == (N,)
+    assert labels.min() >= 0 and labels.max() < k
+
+    assert int(counts.sum()) == N
+    np.testing.assert_array_equal(np.bincount(labels, minlength=k), counts)
+
+    nz = counts > 0
+    tot = (counts[nz, None].astype(np.float64) * C1[nz]).sum(axis=0)
+    # |x| <= ~15 per feature: float64 sums of 1e8 such values agree to ~1e-7
+    np.testing.assert_allclose(tot, sx, rtol=1e-9, atol=1e-3)
+
+    pred = eng.predict()                      # current centroids are still C0
+    np.testing.assert_array_equal(pred, labels)
+
+    gidx = np.sort(np.random.default_rng(7).choice(N, sample, replace=False))
+    Xs = run.rows(gidx.tolist())
+    lab_ref, _, _ = orc.assign(np.asarray(Xs, dtype=np.float64), C0, chunk=chunk)
+    np.testing.assert_array_equal(labels[gidx], lab_ref)
+    assert np.isfinite(st.sse) and st.sse > 0
