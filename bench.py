@@ -156,7 +156,8 @@ def main():
         try:
             tj = json.load(open(args.traffic))
             if tj.get("config") == args.config and tj.get("kernel") == dom:
-                traffic = tj.get("bytes_per_launch")
+                # measured on one GPU holding all N rows; a rank's launch covers n_local
+                traffic = tj.get("bytes_per_launch") * n_local / N
         except Exception:
             traffic = None
     if info["path"] == 2 and dom == "assign":
