@@ -1,6 +1,6 @@
 """c2 small path: assign kernel with fused float64 statistics (Lloyd step) vs
 the same kernel without them (predict), HIP-event averages.  Shows how much of
-k_assign_small is the LDS statistics table.  Usage: python scripts/small_probe.py"""
+k_assign_small is the LDS statistics table.  Usage: python scripts/small_probe.py [config] [N]"""
 import os
 import sys
 
@@ -12,6 +12,8 @@ from kmeans_amd.comm import Communicator  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
 N, d, k, centers = bench.CONFIGS[cfg]
+if len(sys.argv) > 2:                         # row count override (steady state vs launch ramp)
+    N = int(sys.argv[2])
 km = kmeans_amd.KMeans(k=k, max_iter=10 ** 9, tolerance=1e-300, seed=42, compute_sse=False)
 km.verbose = False
 data = kmeans_amd.DeviceBlobs(n=N, d=d, n_centers=centers, box=10.0, std=1.0, seed=2024)
