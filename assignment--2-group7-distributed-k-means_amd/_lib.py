@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(HERE, "libkmeans_amd.so")
 ROOT = os.path.dirname(HERE)
 HEADER = os.path.join(ROOT, "include", "kmeans_amd.h")
 
+KM_ABI_VERSION = 2
 KM_OK = 0
 KM_EMPTY = 1
 
@@ -58,8 +59,7 @@ SIGNATURES = {
     "km_load_rows": [_P, _I64, _PF, _I64],
     "km_generate_blobs": [_P, _I64, _I32, _I64, _I32, ctypes.c_float, ctypes.c_float, ctypes.c_uint64],
     "km_sum_x": [_P, _PD],
-    "km_sq_dev": [_P, _PD, _PD],
-    "km_set_sse_base": [_P, _D],
+    "km_set_sse": [_P, _I32],
     "km_set_centroids": [_P, _PD, _I32, _I32],
     "km_get_centroids": [_P, _I32, _PD],
     "km_assign_stats": [_P],

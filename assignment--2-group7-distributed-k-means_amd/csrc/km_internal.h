@@ -43,8 +43,10 @@ struct Geometry {
 };
 
 // ---- launchers (km_kernels.hip) -------------------------------------------
+// C64P: float64 centroids padded to [kp][dp] (zero padding), the source of
+// the SSE residuals (aligned rows, no per-feature bound checks)
 hipError_t launch_prep_centroids(const double* C64, const Geometry& g, float* C32, float* cn2, float* cmax,
-                                 float* cabs, double* C64T, hipStream_t s);
+                                 float* cabs, double* C64T, double* C64P, hipStream_t s);
 // fp16 hi/lo split of -2*c*s and ||c||^2 s^2 for the MFMA screen (s from the
 // data and centroid abs maxima)
 hipError_t launch_prep_split(const float* C32, const Geometry& g, const float* cn2, const float* xabs,
@@ -52,8 +54,10 @@ hipError_t launch_prep_split(const float* C32, const Geometry& g, const float* c
 hipError_t launch_absmax(const float* X, int64_t nfloats, float* out, hipStream_t s);
 // Small k*d path: direct-form fp32 screening, in-thread exact re-rank,
 // optional fused statistics (LDS float64 table, replicated per lane).
+// want_sse: also add every point's float64 residual ||x - c_label||^2 to
+// stats[k (d+1)] (the SSE slot, kmeans_spark.py:224-237)
 hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C32, const double* C64,
-                               const float* cmax, int32_t* labels, double* stats, int fuse_stats,
+                               const float* cmax, int32_t* labels, double* stats, int fuse_stats, int want_sse,
                                int n_cu, hipStream_t s);
 bool small_path_ok(const Geometry& g);
 // MFMA path: fp16x3 screening on v_mfma_f32_32x32x16_f16, top-3 keys,
@@ -74,7 +78,13 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
 // lo image + float64 sum table in LDS; decided points summed here, queued
 // points (and their counts) by launch_resolve(stats).
 bool fused_path_ok(const Geometry& g);
-void dump_fused_stamps();  // diagnostic (KM_ABLATE=7)
+#ifdef KM_DIAG
+void dump_fused_stamps();  // diagnostic build only (KM_ABLATE=7)
+#endif
+// Tuning / ablation knob `name`: read from the environment only in the
+// diagnostic build (make diag, -DKM_DIAG); the product library always uses
+// `dflt`, so kernel selection depends on the geometry alone.
+int diag_env(const char* name, int dflt);
 hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, const _Float16* Chi,
                         const _Float16* Clo, uint4* ChiF, uint4* CloF, const float* cn2s, const float* bnd,
                         const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,
@@ -86,15 +96,20 @@ hipError_t launch_row_norm(const float* X, const Geometry& g, float* xnorm, hipS
 // once); scratch = sorted_stats_words(n, k) uint32 words
 bool stats_needs_sort(const Geometry& g);
 size_t sorted_stats_words(int64_t n, int k);
+// C64P != nullptr: the SSE residuals are accumulated in the same pass
 hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t* labels, double* stats,
-                               uint32_t* scratch, int n_cu, hipStream_t s);
+                               uint32_t* scratch, const double* C64P, int n_cu, hipStream_t s);
 hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels, double* stats, int n_cu,
                         hipStream_t s);
-hipError_t launch_update(const double* stats, const double* C64_old, const double* mu, const Geometry& g,
-                         double* C64_new, double* work, int64_t* counts, const double* sse_base,
-                         const uint32_t* qcount, uint32_t nq, DevStatus* status, hipStream_t s);
+// SSE of the final labels (kmeans_spark.py:224-237): sum over rows of the
+// float64 residual ||x - c_label||^2, added to *sse (one atomic per wave)
+hipError_t launch_sse(const float* X, const Geometry& g, const int32_t* labels, const double* C64P, double* sse,
+                      hipStream_t s);
+// stats = [k][d+1] sums and counts, then the SSE slot stats[k (d+1)]
+hipError_t launch_update(const double* stats, const double* C64_old, const Geometry& g, double* C64_new,
+                         double* work, int64_t* counts, const uint32_t* qcount, uint32_t nq, DevStatus* status,
+                         hipStream_t s);
 hipError_t launch_sum_x(const float* X, const Geometry& g, double* out, hipStream_t s);
-hipError_t launch_sq_dev(const float* X, const Geometry& g, const double* mu, double* out, hipStream_t s);
 hipError_t launch_gather_rows(const float* X, const Geometry& g, const int64_t* idx, int32_t n, double* out,
                               hipStream_t s);
 // takeSample's Bernoulli pass, one wave per partition (km_sample.hip)

@@ -90,7 +90,7 @@ __host__ __device__ inline float screen_b0(float xn_s, float cm_s, float pm_s, i
 __global__ __launch_bounds__(64) void k_prep_centroids(const double* __restrict__ C64, int k, int d, int dp,
                                                        float* __restrict__ C32, float* __restrict__ cn2,
                                                        float* __restrict__ cmax, float* __restrict__ cabs,
-                                                       double* __restrict__ C64T) {
+                                                       double* __restrict__ C64T, double* __restrict__ C64P) {
   const int j = blockIdx.x;
   const int lane = threadIdx.x;
   double nn = 0.0;
@@ -98,6 +98,7 @@ __global__ __launch_bounds__(64) void k_prep_centroids(const double* __restrict_
   for (int f = lane; f < dp; f += 64) {
     const double c = (j < k && f < d) ? C64[(size_t)j * d + f] : 0.0;
     if (j < k && f < d) C64T[(size_t)f * k + j] = c;
+    C64P[(size_t)j * dp + f] = c;
     nn = fma(c, c, nn);
     const float c32 = (float)c;
     C32[(size_t)j * dp + f] = c32;
@@ -120,12 +121,13 @@ __global__ __launch_bounds__(64) void k_prep_centroids(const double* __restrict_
 }
 
 hipError_t launch_prep_centroids(const double* C64, const Geometry& g, float* C32, float* cn2, float* cmax,
-                                 float* cabs, double* C64T, hipStream_t s) {
+                                 float* cabs, double* C64T, double* C64P, hipStream_t s) {
   hipError_t e = hipMemsetAsync(cmax, 0, sizeof(float), s);
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(cabs, 0, sizeof(float), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_prep_centroids, dim3(g.kp), dim3(64), 0, s, C64, g.k, g.d, g.dp, C32, cn2, cmax, cabs, C64T);
+  hipLaunchKernelGGL(k_prep_centroids, dim3(g.kp), dim3(64), 0, s, C64, g.k, g.d, g.dp, C32, cn2, cmax, cabs, C64T,
+                     C64P);
   return hipGetLastError();
 }
 
@@ -146,7 +148,7 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
                                                       const float* __restrict__ C32,
                                                       const double* __restrict__ C64,
                                                       const float* __restrict__ cmaxp, int32_t* __restrict__ labels,
-                                                      double* __restrict__ stats, int fuse, int R) {
+                                                      double* __restrict__ stats, int fuse, int want_sse, int R) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* sC = reinterpret_cast<float*>(smem);
   double* tab = reinterpret_cast<double*>(smem + ((k * DP * 4 + 15) / 16) * 16);
@@ -176,6 +178,7 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
   // while this one is processed (the loop is otherwise latency-bound)
   const int64_t rstride = (int64_t)gridDim.x * blockDim.x;
   int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double sacc = 0.0;  // this lane's SSE residuals (want_sse)
   float4 nx[DP / 4];
   if (row < n) {
 #pragma unroll
@@ -243,6 +246,20 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
     }
     if (lab >= k) lab = 0;  // only reachable with non-finite data (np.argmin of NaNs -> 0)
     labels[row] = lab;
+    if (want_sse) {
+      // min(norm)**2 of compute_partition_sse (kmeans_spark.py:231-233): the
+      // residual to the pre-update centroid, each difference and square in
+      // float64 (no cancellation, unlike ||x||^2 - 2 x.c + ||c||^2)
+      const double* c = C64 + (size_t)lab * d;
+      double r = 0.0;
+#pragma unroll
+      for (int f = 0; f < DP; ++f)
+        if (f < d) {
+          const double t = (double)x[f] - c[f];
+          r = fma(t, t, r);
+        }
+      sacc += r;
+    }
     if (fuse) {
       double* t = tab + (size_t)lab * d1 * R + rep;
 #pragma unroll
@@ -250,6 +267,10 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
         if (f < d) atomicAdd(t + (size_t)f * R, (double)x[f]);
       atomicAdd(t + (size_t)d * R, 1.0);
     }
+  }
+  if (want_sse) {
+    sacc = wave_sum(sacc);
+    if ((threadIdx.x & 63) == 0 && sacc != 0.0) atomicAdd(stats + (size_t)k * d1, sacc);
   }
   if (fuse) {
     __syncthreads();
@@ -261,15 +282,21 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
   }
 }
 
-// tuning knobs (defaults measured on MI355X; env overrides for sweeps)
-static int small_env(const char* name, int dflt) {
+// tuning knobs: defaults measured on MI355X; environment overrides exist only
+// in the diagnostic build (make diag) for sweeps and ablations
+int diag_env(const char* name, int dflt) {
+#ifdef KM_DIAG
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
 }
 
 static int small_replicas(const Geometry& g) {
   const size_t cbytes = ((size_t)g.k * g.dp * 4 + 15) / 16 * 16;
-  static const int rmax = small_env("KM_SMALL_R", 32);
+  static const int rmax = diag_env("KM_SMALL_R", 32);
   int R = rmax;
   while (R > 1 && cbytes + (size_t)g.k * (g.d + 1) * 8 * R > SMALL_LDS) R >>= 1;
   return R;
@@ -282,31 +309,31 @@ bool small_path_ok(const Geometry& g) {
 }
 
 hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C32, const double* C64,
-                               const float* cmax, int32_t* labels, double* stats, int fuse, int n_cu,
+                               const float* cmax, int32_t* labels, double* stats, int fuse, int want_sse, int n_cu,
                                hipStream_t s) {
   if (g.n == 0) return hipSuccess;
   const int R = small_replicas(g);
   const size_t lds = ((size_t)g.k * g.dp * 4 + 15) / 16 * 16 + (fuse ? (size_t)g.k * (g.d + 1) * 8 * R : 0);
   int64_t blocks = (g.n + 255) / 256;
-  static const int bpc = small_env("KM_SMALL_BPC", 4);
+  static const int bpc = diag_env("KM_SMALL_BPC", 4);
   const int64_t cap = (int64_t)n_cu * bpc;
   if (blocks > cap) blocks = cap;
   switch (g.dp) {
     case 16:
       hipLaunchKernelGGL(k_assign_small<16>, dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d, g.k, C32, C64,
-                         cmax, labels, stats, fuse, R);
+                         cmax, labels, stats, fuse, want_sse, R);
       break;
     case 32:
       hipLaunchKernelGGL(k_assign_small<32>, dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d, g.k, C32, C64,
-                         cmax, labels, stats, fuse, R);
+                         cmax, labels, stats, fuse, want_sse, R);
       break;
     case 48:
       hipLaunchKernelGGL(k_assign_small<48>, dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d, g.k, C32, C64,
-                         cmax, labels, stats, fuse, R);
+                         cmax, labels, stats, fuse, want_sse, R);
       break;
     case 64:
       hipLaunchKernelGGL(k_assign_small<64>, dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d, g.k, C32, C64,
-                         cmax, labels, stats, fuse, R);
+                         cmax, labels, stats, fuse, want_sse, R);
       break;
     default:
       return hipErrorInvalidValue;
@@ -688,11 +715,7 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
 }
 
 static int mfma_waves_env() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("KM_MFMA_WAVES");  // experiment knob: 12 (default) or 8
-    v = (e && e[0] == '8') ? 8 : 12;
-  }
+  static const int v = diag_env("KM_MFMA_WAVES", 12) == 8 ? 8 : 12;  // experiment knob: 12 (default) or 8
   return v;
 }
 
@@ -725,7 +748,7 @@ hipError_t launch_prep_split(const float* C32, const Geometry& g, const float* c
 }
 
 static int mfma_top2(int ns) {
-  static const int e = small_env("KM_TOP2", -1);  // -1: by d (key-update-bound shapes), 0/1: force
+  static const int e = diag_env("KM_TOP2", -1);  // -1: by d (key-update-bound shapes), 0/1: force
   return e >= 0 ? e : (ns <= 2 ? 1 : 0);
 }
 
@@ -751,15 +774,15 @@ static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, con
       hipLaunchKernelGGL((k_assign_mfma<NS, 12>), dim3(blocks), dim3(768), lds, s, a);
     else
       hipLaunchKernelGGL((k_assign_mfma<NS, 8>), dim3(blocks), dim3(512), lds, s, a);
+#ifdef KM_DIAG
     if constexpr (NS == 4) {  // diagnostic ablations (KM_ABLATE=1|2), c3 shape only
-      static const char* e = getenv("KM_ABLATE");
-      if (e && (e[0] == '1' || e[0] == '2')) {
-        if (e[0] == '1')
-          hipLaunchKernelGGL((k_assign_mfma<NS, 12, 1>), dim3(blocks), dim3(768), lds, s, a);
-        else
-          hipLaunchKernelGGL((k_assign_mfma<NS, 12, 2>), dim3(blocks), dim3(768), lds, s, a);
-      }
+      static const int e = diag_env("KM_ABLATE", 0);
+      if (e == 1)
+        hipLaunchKernelGGL((k_assign_mfma<NS, 12, 1>), dim3(blocks), dim3(768), lds, s, a);
+      else if (e == 2)
+        hipLaunchKernelGGL((k_assign_mfma<NS, 12, 2>), dim3(blocks), dim3(768), lds, s, a);
     }
+#endif
   }
 }
 
@@ -1329,6 +1352,7 @@ __global__ __launch_bounds__(256) void k_row_norm_any(const float* __restrict__ 
   }
 }
 
+#ifdef KM_DIAG
 // diagnostic: print and clear the ABL=7 phase stamps (cycles summed over waves)
 void dump_fused_stamps() {
   unsigned long long v[8];
@@ -1346,6 +1370,7 @@ void dump_fused_stamps() {
   unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z));
 }
+#endif
 
 bool fused_path_ok(const Geometry& g) {
   const int ns = g.dp / 16, nb = g.kp / 32;
@@ -1391,22 +1416,24 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
     else                                                                                               \
       hipLaunchKernelGGL((k_fused<NS_, NB_, false>), dim3(nbk), dim3(256), lds, s, a);                 \
     break;
+#ifdef KM_DIAG
   {
-    static const char* abl = getenv("KM_ABLATE");
-    if (abl && ns == 4 && nb == 8 && with_stats && abl[0] >= '1' && abl[0] <= '8') {
-      switch (abl[0]) {
-        case '1': hipLaunchKernelGGL((k_fused<4, 8, true, 1>), dim3(nbk), dim3(256), lds, s, a); break;
-        case '2': hipLaunchKernelGGL((k_fused<4, 8, true, 2>), dim3(nbk), dim3(256), lds, s, a); break;
-        case '3': hipLaunchKernelGGL((k_fused<4, 8, true, 3>), dim3(nbk), dim3(256), lds, s, a); break;
-        case '5': hipLaunchKernelGGL((k_fused<4, 8, true, 5>), dim3(nbk), dim3(256), lds, s, a); break;
-        case '7': hipLaunchKernelGGL((k_fused<4, 8, true, 7>), dim3(nbk), dim3(256), lds, s, a); break;
-        case '8': hipLaunchKernelGGL((k_fused<4, 8, true, 8>), dim3(nbk), dim3(256), lds, s, a); break;
-        case '6': hipLaunchKernelGGL((k_fused<4, 8, true, 6>), dim3(nbk), dim3(256), lds, s, a); break;
+    static const int abl = diag_env("KM_ABLATE", 0);
+    if (abl >= 1 && abl <= 8 && ns == 4 && nb == 8 && with_stats) {
+      switch (abl) {
+        case 1: hipLaunchKernelGGL((k_fused<4, 8, true, 1>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 2: hipLaunchKernelGGL((k_fused<4, 8, true, 2>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 3: hipLaunchKernelGGL((k_fused<4, 8, true, 3>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 5: hipLaunchKernelGGL((k_fused<4, 8, true, 5>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 7: hipLaunchKernelGGL((k_fused<4, 8, true, 7>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 8: hipLaunchKernelGGL((k_fused<4, 8, true, 8>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 6: hipLaunchKernelGGL((k_fused<4, 8, true, 6>), dim3(nbk), dim3(256), lds, s, a); break;
         default: hipLaunchKernelGGL((k_fused<4, 8, true, 4>), dim3(nbk), dim3(256), lds, s, a); break;
       }
       return hipGetLastError();
     }
   }
+#endif
   switch (ns * 100 + nb) {
     KM_FUSED_CASE(4, 2) KM_FUSED_CASE(4, 4) KM_FUSED_CASE(4, 6) KM_FUSED_CASE(4, 8)
     KM_FUSED_CASE(2, 2) KM_FUSED_CASE(2, 4) KM_FUSED_CASE(2, 6) KM_FUSED_CASE(2, 8) KM_FUSED_CASE(2, 12)
@@ -1793,14 +1820,14 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   if (g.d > 256) return hipErrorInvalidValue;
   // full / chain scans first (labels only); k_rerank2 then adds the sums of
   // both queues through its LDS table
-  static const int fs_g = small_env("KM_FS_G", 2);  // entries per wave: 2 or 4
+  static const int fs_g = diag_env("KM_FS_G", 2);  // entries per wave: 2 or 4
   const int G = fs_g == 4 ? 4 : 2;
   const int ch = g.d <= 128 ? 64 : 32;  // chunk columns: <= 64 KiB of LDS
   const size_t fs_lds = (size_t)g.d * ch * 8 + (size_t)8 * G * g.d * 4 + pre_bytes;
   if (fs_lds > LDS_MAX) return hipErrorInvalidValue;
-  static const int use_chain = small_env("KM_CHAIN", 1);
-  static const int pair_chain = small_env("KM_PAIR_CHAIN", 1);
-  static const int fs_wg = small_env("KM_FS_WG", 1);  // workgroups per CU (3: no measurable change)
+  static const int use_chain = diag_env("KM_CHAIN", 1);
+  static const int pair_chain = diag_env("KM_PAIR_CHAIN", 1);
+  static const int fs_wg = diag_env("KM_FS_WG", 1);  // workgroups per CU (3: no measurable change)
   if (G == 4)
     hipLaunchKernelGGL(k_fullscan<4>, dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T, queue,
                        qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain);
@@ -2016,17 +2043,21 @@ __global__ __launch_bounds__(256) void k_scatter(const int32_t* __restrict__ lab
 // in one cluster, flushing it with global float64 atomics (contiguous 16 B
 // per lane) when the cluster changes and at the end.  Counts come from the
 // histogram.
+// With C64P the SSE residuals ride along: the sorted order keeps a lane's
+// centroid features constant over a run, so they are reloaded only when the
+// cluster changes.
 template <int L>  // lanes per row = dp / 4
 __global__ __launch_bounds__(256) void k_segsum(const float* __restrict__ X, int d, int64_t n,
                                                 const uint32_t* __restrict__ perm, const int32_t* __restrict__ slab,
-                                                double* __restrict__ stats) {
+                                                double* __restrict__ stats, const double* __restrict__ C64P,
+                                                double* __restrict__ sse) {
   constexpr int P = 64 / L;  // rows per wave-instruction
   constexpr int U = 4;       // instructions in flight
   constexpr int DP = 4 * L;
   const int lane = threadIdx.x & 63;
   const int q = lane / L;
   const int m = lane % L;
-  if (q >= P) return;  // dp = 48, 96, 192: the lanes past the last whole row idle (no barriers here)
+  const bool act = q < P;  // dp = 48, 96, 192: the lanes past the last whole row idle
   const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int64_t per = (n + nw - 1) / nw;
@@ -2035,6 +2066,7 @@ __global__ __launch_bounds__(256) void k_segsum(const float* __restrict__ X, int
   const int d1 = d + 1;
   int cur = -1;
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0, ss = 0.0;
   auto flush = [&]() {
     if (cur >= 0) {
       double* o = stats + (size_t)cur * d1 + 4 * m;
@@ -2045,7 +2077,7 @@ __global__ __launch_bounds__(256) void k_segsum(const float* __restrict__ X, int
     }
     a0 = a1 = a2 = a3 = 0.0;
   };
-  for (int64_t base = p0; base < p1; base += P * U) {
+  for (int64_t base = p0; act && base < p1; base += P * U) {
     float4 v[U];
     int lb[U];
 #pragma unroll
@@ -2066,14 +2098,105 @@ __global__ __launch_bounds__(256) void k_segsum(const float* __restrict__ X, int
       if (lb[u] != cur) {
         flush();
         cur = lb[u];
+        if (C64P) {
+          const double2 ca = *reinterpret_cast<const double2*>(C64P + (size_t)cur * DP + 4 * m);
+          const double2 cb = *reinterpret_cast<const double2*>(C64P + (size_t)cur * DP + 4 * m + 2);
+          c0 = ca.x;
+          c1 = ca.y;
+          c2 = cb.x;
+          c3 = cb.y;
+        }
       }
       a0 += (double)v[u].x;
       a1 += (double)v[u].y;
       a2 += (double)v[u].z;
       a3 += (double)v[u].w;
+      if (C64P) {  // padded features are 0 - 0
+        const double t0 = (double)v[u].x - c0, t1 = (double)v[u].y - c1;
+        const double t2 = (double)v[u].z - c2, t3 = (double)v[u].w - c3;
+        ss = fma(t0, t0, ss);
+        ss = fma(t1, t1, ss);
+        ss = fma(t2, t2, ss);
+        ss = fma(t3, t3, ss);
+      }
     }
   }
-  flush();
+  if (act) flush();
+  if (C64P) {
+    ss = wave_sum(ss);
+    if (lane == 0 && ss != 0.0) atomicAdd(sse, ss);
+  }
+}
+
+// SSE of the final labels (kmeans_spark.py:224-237) where no statistics pass
+// carries it: L = dp/4 lanes per row (float4 each), P = 64/L rows per
+// wave-instruction, U rows in flight per lane; the centroid features come
+// from the padded float64 copy (L2-resident) by label.
+template <int L>
+__global__ __launch_bounds__(256) void k_sse(const float* __restrict__ X, int64_t n,
+                                             const int32_t* __restrict__ labels, const double* __restrict__ C64P,
+                                             double* __restrict__ sse) {
+  constexpr int P = 64 / L;
+  constexpr int U = 4;
+  constexpr int DP = 4 * L;
+  const int lane = threadIdx.x & 63;
+  const int q = lane / L;
+  const int m = lane % L;
+  const bool act = q < P;
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  double ss = 0.0;
+  for (int64_t r0 = gw * (P * U); act && r0 < n; r0 += nw * (P * U)) {
+    float4 v[U];
+    int lb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = r0 + u * P + q;
+      if (row < n) {
+        lb[u] = labels[row];
+        v[u] = *reinterpret_cast<const float4*>(X + (size_t)row * DP + 4 * m);
+      } else {
+        lb[u] = -1;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (lb[u] < 0) continue;
+      const double* c = C64P + (size_t)lb[u] * DP + 4 * m;
+      const double2 ca = *reinterpret_cast<const double2*>(c);
+      const double2 cb = *reinterpret_cast<const double2*>(c + 2);
+      const double t0 = (double)v[u].x - ca.x, t1 = (double)v[u].y - ca.y;
+      const double t2 = (double)v[u].z - cb.x, t3 = (double)v[u].w - cb.y;
+      ss = fma(t0, t0, ss);
+      ss = fma(t1, t1, ss);
+      ss = fma(t2, t2, ss);
+      ss = fma(t3, t3, ss);
+    }
+  }
+  ss = wave_sum(ss);
+  if (lane == 0 && ss != 0.0) atomicAdd(sse, ss);
+}
+
+hipError_t launch_sse(const float* X, const Geometry& g, const int32_t* labels, const double* C64P, double* sse,
+                      hipStream_t s) {
+  if (g.n == 0) return hipSuccess;
+  const int L = g.dp / 4;
+  const int P = 64 / L;
+  int64_t blocks = (g.n + 4 * P * 4 - 1) / (4 * P * 4);  // 4 waves per block, P*4 rows per wave-step
+  if (blocks > 8192) blocks = 8192;
+  const dim3 grid((unsigned)blocks), blk(256);
+  switch (L) {
+    case 4: hipLaunchKernelGGL(k_sse<4>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
+    case 8: hipLaunchKernelGGL(k_sse<8>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
+    case 12: hipLaunchKernelGGL(k_sse<12>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
+    case 16: hipLaunchKernelGGL(k_sse<16>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
+    case 24: hipLaunchKernelGGL(k_sse<24>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
+    case 32: hipLaunchKernelGGL(k_sse<32>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
+    case 48: hipLaunchKernelGGL(k_sse<48>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
+    case 64: hipLaunchKernelGGL(k_sse<64>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 // counts of the histogram into the count column
@@ -2089,14 +2212,14 @@ size_t sorted_stats_words(int64_t n, int k) { return 2 * (size_t)n + 3 * (size_t
 // label/permutation traffic, and cursor atomics that contend when k is small)
 // is cheaper
 bool stats_needs_sort(const Geometry& g) {
-  static const int min_ranges = small_env("KM_SORT_MIN_RANGES", 3);  // A/B knob
+  static const int min_ranges = diag_env("KM_SORT_MIN_RANGES", 3);  // A/B knob
   int fr = 0, kr = 0;
   stats_ranges(g, &fr, &kr);
   return kr == 0 || (g.k + kr - 1) / kr >= min_ranges;
 }
 
 hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t* labels, double* stats,
-                               uint32_t* scratch, int n_cu, hipStream_t s) {
+                               uint32_t* scratch, const double* C64P, int n_cu, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
   if (g.dp > 256) return hipErrorInvalidValue;
   uint32_t* cnt = scratch;
@@ -2122,14 +2245,14 @@ hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t*
   int64_t wb = (int64_t)n_cu * 8;
   const unsigned grid = (unsigned)wb;
   switch (g.dp / 4) {
-    case 4: hipLaunchKernelGGL(k_segsum<4>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
-    case 8: hipLaunchKernelGGL(k_segsum<8>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
-    case 12: hipLaunchKernelGGL(k_segsum<12>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
-    case 16: hipLaunchKernelGGL(k_segsum<16>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
-    case 24: hipLaunchKernelGGL(k_segsum<24>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
-    case 32: hipLaunchKernelGGL(k_segsum<32>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
-    case 48: hipLaunchKernelGGL(k_segsum<48>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
-    case 64: hipLaunchKernelGGL(k_segsum<64>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats); break;
+    case 4: hipLaunchKernelGGL(k_segsum<4>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
+    case 8: hipLaunchKernelGGL(k_segsum<8>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
+    case 12: hipLaunchKernelGGL(k_segsum<12>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
+    case 16: hipLaunchKernelGGL(k_segsum<16>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
+    case 24: hipLaunchKernelGGL(k_segsum<24>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
+    case 32: hipLaunchKernelGGL(k_segsum<32>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
+    case 48: hipLaunchKernelGGL(k_segsum<48>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
+    case 64: hipLaunchKernelGGL(k_segsum<64>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -2138,19 +2261,17 @@ hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t*
 // ---------------------------------------------------------------------------
 // Centroid update (kmeans_spark.py:176-206 + 278-294): new = sum / count,
 // empties keep the old centroid (host replaces them, L191-204), per-cluster
-// squared shift, SSE via the closed form
-//   SSE = sum_p ||x_p - mu||^2 - 2 sum_j (c_j - mu).(S_j - n_j mu) + sum_j n_j ||c_j - mu||^2
-// with c_j the PRE-update centroids (L279 uses centroids_bc).
+// squared shift.  The SSE (L224-237) is the all-reduced residual slot
+// stats[k (d+1)] filled by the assign / statistics passes.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_update(const double* __restrict__ stats, const double* __restrict__ old,
-                                               const double* __restrict__ mu, int k, int d,
-                                               double* __restrict__ out, double* __restrict__ work,
+                                               int k, int d, double* __restrict__ out, double* __restrict__ work,
                                                int64_t* __restrict__ counts) {
   const int j = blockIdx.x;
   const int lane = threadIdx.x;
   const int d1 = d + 1;
   const double cnt = stats[(size_t)j * d1 + d];
-  double sh = 0.0, t = 0.0, nf = 0.0;
+  double sh = 0.0, nf = 0.0;
   for (int f = lane; f < d; f += 64) {
     const double S = stats[(size_t)j * d1 + f];
     const double o = old[(size_t)j * d + f];
@@ -2159,29 +2280,23 @@ __global__ __launch_bounds__(64) void k_update(const double* __restrict__ stats,
     const double df = nv - o;
     sh = fma(df, df, sh);
     if (!isfinite(nv)) nf = 1.0;
-    if (cnt > 0.0) {
-      const double cmu = o - mu[f];
-      t += -2.0 * cmu * (S - cnt * mu[f]) + cnt * cmu * cmu;
-    }
   }
   sh = wave_sum(sh);
-  t = wave_sum(t);
   nf = wave_sum(nf);
   if (lane == 0) {
     work[j] = sh;
-    work[k + j] = t;
     work[2 * k + j] = nf;
     counts[j] = (int64_t)cnt;
   }
 }
 
 __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ work, const int64_t* __restrict__ counts,
-                                                  int k, const double* __restrict__ sse_base,
+                                                  int k, const double* __restrict__ sse,
                                                   const uint32_t* __restrict__ qcount, uint32_t nq,
                                                   DevStatus* __restrict__ st) {
-  __shared__ double s_max[256], s_sum[256];
+  __shared__ double s_max[256];
   __shared__ int s_emp[256], s_nf[256], s_q[256], s_qf[256];
-  double mx = 0.0, sm = 0.0;
+  double mx = 0.0;
   int emp = 0, nf = 0, qa = 0, qb = 0;
   for (uint32_t w = threadIdx.x; w < nq; w += 256) {
     qa += (int)qcount[2 * w];
@@ -2191,19 +2306,16 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ wor
   s_qf[threadIdx.x] = qb;
   for (int j = threadIdx.x; j < k; j += 256) {
     mx = fmax(mx, work[j]);
-    sm += work[k + j];
     nf |= (work[2 * k + j] != 0.0);
     emp += (counts[j] == 0);
   }
   s_max[threadIdx.x] = mx;
-  s_sum[threadIdx.x] = sm;
   s_emp[threadIdx.x] = emp;
   s_nf[threadIdx.x] = nf;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if (threadIdx.x < o) {
       s_max[threadIdx.x] = fmax(s_max[threadIdx.x], s_max[threadIdx.x + o]);
-      s_sum[threadIdx.x] += s_sum[threadIdx.x + o];
       s_emp[threadIdx.x] += s_emp[threadIdx.x + o];
       s_nf[threadIdx.x] |= s_nf[threadIdx.x + o];
       s_q[threadIdx.x] += s_q[threadIdx.x + o];
@@ -2213,7 +2325,7 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ wor
   }
   if (threadIdx.x == 0) {
     st->max_shift = sqrt(s_max[0]);
-    st->sse = *sse_base + s_sum[0];
+    st->sse = *sse;
     st->n_empty = s_emp[0];
     st->nonfinite = s_nf[0];
     st->q_full = s_qf[0];
@@ -2221,18 +2333,19 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ wor
   }
 }
 
-hipError_t launch_update(const double* stats, const double* C64_old, const double* mu, const Geometry& g,
-                         double* C64_new, double* work, int64_t* counts, const double* sse_base,
-                         const uint32_t* qcount, uint32_t nq, DevStatus* status, hipStream_t s) {
-  hipLaunchKernelGGL(k_update, dim3(g.k), dim3(64), 0, s, stats, C64_old, mu, g.k, g.d, C64_new, work, counts);
+hipError_t launch_update(const double* stats, const double* C64_old, const Geometry& g, double* C64_new,
+                         double* work, int64_t* counts, const uint32_t* qcount, uint32_t nq, DevStatus* status,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_update, dim3(g.k), dim3(64), 0, s, stats, C64_old, g.k, g.d, C64_new, work, counts);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, work, counts, g.k, sse_base, qcount, nq, status);
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, work, counts, g.k, stats + (size_t)g.k * (g.d + 1),
+                     qcount, nq, status);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
-// Data moments (once per load): sum_p x_p and sum_p ||x_p - mu||^2, float64.
+// Data moment (checks): sum_p x_p, float64.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_sum_x(const float* __restrict__ X, int64_t n, int d, int dp,
                                                double* __restrict__ out) {
@@ -2248,41 +2361,11 @@ __global__ __launch_bounds__(256) void k_sum_x(const float* __restrict__ X, int6
   }
 }
 
-__global__ __launch_bounds__(256) void k_sq_dev(const float* __restrict__ X, int64_t n, int d, int dp,
-                                                const double* __restrict__ mu, double* __restrict__ out) {
-  __shared__ double red[4];
-  const int fl = threadIdx.x & 63;
-  const int rg = threadIdx.x >> 6;
-  double acc = 0.0;
-  for (int f0 = 0; f0 < d; f0 += 64) {
-    const int f = f0 + fl;
-    if (f < d) {
-      const double m = mu[f];
-      for (int64_t row = (int64_t)blockIdx.x * 4 + rg; row < n; row += (int64_t)gridDim.x * 4) {
-        const double t = (double)X[row * dp + f] - m;
-        acc = fma(t, t, acc);
-      }
-    }
-  }
-  acc = wave_sum(acc);
-  if (fl == 0) red[rg] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
-}
-
 hipError_t launch_sum_x(const float* X, const Geometry& g, double* out, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
   int64_t blocks = (g.n + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(k_sum_x, dim3((unsigned)blocks), dim3(256), 0, s, X, g.n, g.d, g.dp, out);
-  return hipGetLastError();
-}
-
-hipError_t launch_sq_dev(const float* X, const Geometry& g, const double* mu, double* out, hipStream_t s) {
-  if (g.n == 0) return hipSuccess;
-  int64_t blocks = (g.n + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(k_sq_dev, dim3((unsigned)blocks), dim3(256), 0, s, X, g.n, g.d, g.dp, mu, out);
   return hipGetLastError();
 }
 

@@ -48,12 +48,12 @@ void hfree(T*& p) {
 
 constexpr int kAllowedDp[] = {16, 32, 48, 64, 96, 128, 192, 256};
 
-// KM_FUSED=0 selects the two-pass MFMA path (screen, then a statistics pass)
-// for the shapes the fused kernel covers (A/B measurements)
-bool fused_disabled() {
-  const char* e = getenv("KM_FUSED");
-  return e && e[0] == '0';
-}
+// KM_FUSED=0 (diagnostic build only) selects the two-pass MFMA path (screen,
+// then a statistics pass) for the shapes the fused kernel covers (A/B runs)
+bool fused_disabled() { return km::diag_env("KM_FUSED", 1) == 0; }
+
+// [k][d+1] sums and counts, then the SSE slot
+size_t stats_len(const km::Geometry& g) { return (size_t)g.k * (g.d + 1) + 1; }
 
 int choose_dp(int d) {
   for (int v : kAllowedDp)
@@ -79,8 +79,7 @@ struct km_ctx {
   uint32_t* qcount = nullptr;
   km::QLayout ql{0, 0};
   double* moments = nullptr;  // d+1 scratch
-  double* mu = nullptr;       // d
-  double* sse_base = nullptr; // 1
+  bool want_sse = false;      // km_set_sse: SSE residuals in km_assign_stats
   int64_t* idx_scratch = nullptr;
   double* rows_scratch = nullptr;
   int64_t scratch_rows = 0;
@@ -89,6 +88,7 @@ struct km_ctx {
   double* C64_cur = nullptr;
   double* C64_new = nullptr;
   double* C64T = nullptr;  // transposed [d][k] (full exact scans)
+  double* C64P = nullptr;  // padded [kp][dp] (SSE residuals)
   float* C32 = nullptr;
   _Float16* Chi = nullptr;  // fp16 hi/lo of -2*c*s [kp][dp]
   _Float16* Clo = nullptr;
@@ -156,6 +156,7 @@ void free_centroids(km_ctx* c) {
   dfree(c->C64_cur);
   dfree(c->C64_new);
   dfree(c->C64T);
+  dfree(c->C64P);
   dfree(c->C32);
   dfree(c->Chi);
   dfree(c->Clo);
@@ -190,8 +191,6 @@ void free_data(km_ctx* c) {
   dfree(c->xnorm);
   dfree(c->sort_scratch);
   c->sort_words = 0;
-  dfree(c->mu);
-  dfree(c->sse_base);
   dfree(c->idx_scratch);
   dfree(c->rows_scratch);
   c->scratch_rows = 0;
@@ -204,7 +203,7 @@ void free_data(km_ctx* c) {
 int prep(km_ctx* c, const double* src) {
   ProfScope ps(c, KM_K_PREP);
   c->prep_of = src;
-  KM_HIP(km::launch_prep_centroids(src, c->g, c->C32, c->cn2, c->cmax, c->cabs, c->C64T, c->stream));
+  KM_HIP(km::launch_prep_centroids(src, c->g, c->C32, c->cn2, c->cmax, c->cabs, c->C64T, c->C64P, c->stream));
   KM_HIP(km::launch_prep_split(c->C32, c->g, c->cn2, c->xabs, c->cabs, c->Chi, c->Clo, c->cn2s, c->stream));
   KM_HIP(km::launch_bound_consts(c->cmax, c->xabs, c->cabs, c->g.dp, c->bnd, c->stream));
   return KM_OK;
@@ -229,11 +228,13 @@ int run_assign(km_ctx* c, bool with_stats) {
     if (rc != KM_OK) return rc;
   }
   c->ql = km::QLayout{0, 0};
-  if (with_stats) KM_HIP(hipMemsetAsync(c->stats, 0, sizeof(double) * (size_t)g.k * (g.d + 1), c->stream));
+  const bool sse = with_stats && c->want_sse;
+  double* sse_slot = c->stats + (size_t)g.k * (g.d + 1);
+  if (with_stats) KM_HIP(hipMemsetAsync(c->stats, 0, sizeof(double) * stats_len(g), c->stream));
   if (c->path == 1) {
     ProfScope ps(c, KM_K_ASSIGN);
     KM_HIP(km::launch_assign_small(c->X, g, c->C32, c->C64_cur, c->cmax, c->labels, c->stats, with_stats ? 1 : 0,
-                                   c->n_cu, c->stream));
+                                   sse ? 1 : 0, c->n_cu, c->stream));
     return KM_OK;
   }
   if (c->fused) {
@@ -247,6 +248,12 @@ int run_assign(km_ctx* c, bool with_stats) {
       ProfScope ps(c, KM_K_RESOLVE);
       KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels,
                                 with_stats ? c->stats : nullptr, c->n_cu, c->stream));
+    }
+    if (sse) {
+      // the fused kernel's LDS holds the sum table: the residuals are a
+      // second pass over the final labels (only when compute_sse)
+      ProfScope ps(c, KM_K_STATS);
+      KM_HIP(km::launch_sse(c->X, g, c->labels, c->C64P, sse_slot, c->stream));
     }
     return KM_OK;  // counts are part of the fused and resolver statistics
   }
@@ -269,9 +276,11 @@ int run_assign(km_ctx* c, bool with_stats) {
         KM_HIP(hipMalloc(&c->sort_scratch, sizeof(uint32_t) * words));
         c->sort_words = words;
       }
-      KM_HIP(km::launch_stats_sorted(c->X, g, c->labels, c->stats, c->sort_scratch, c->n_cu, c->stream));
+      KM_HIP(km::launch_stats_sorted(c->X, g, c->labels, c->stats, c->sort_scratch, sse ? c->C64P : nullptr,
+                                     c->n_cu, c->stream));
     } else {
       KM_HIP(km::launch_stats(c->X, g, c->labels, c->stats, c->n_cu, c->stream));
+      if (sse) KM_HIP(km::launch_sse(c->X, g, c->labels, c->C64P, sse_slot, c->stream));
     }
   }
   return KM_OK;
@@ -349,10 +358,9 @@ int km_sync(km_ctx* c) {
   KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
   KM_HIP(hipSetDevice(c->device));
   KM_HIP(hipStreamSynchronize(c->stream));
-  {
-    static const char* abl = getenv("KM_ABLATE");
-    if (abl && abl[0] == '7') km::dump_fused_stamps();
-  }
+#ifdef KM_DIAG
+  if (km::diag_env("KM_ABLATE", 0) == 7) km::dump_fused_stamps();
+#endif
   return KM_OK;
 }
 
@@ -392,10 +400,6 @@ int km_load_begin(km_ctx* c, int64_t n, int32_t d) {
   KM_HIP(hipMalloc(&c->xabs, sizeof(float)));
   KM_HIP(hipMalloc(&c->xnorm, sizeof(float) * rows));
   KM_HIP(hipMemsetAsync(c->xabs, 0, sizeof(float), c->stream));
-  KM_HIP(hipMalloc(&c->mu, sizeof(double) * d));
-  KM_HIP(hipMemsetAsync(c->mu, 0, sizeof(double) * d, c->stream));
-  KM_HIP(hipMalloc(&c->sse_base, sizeof(double)));
-  KM_HIP(hipMemsetAsync(c->sse_base, 0, sizeof(double), c->stream));
   KM_HIP(hipStreamSynchronize(c->stream));
   c->loaded = true;
   return KM_OK;
@@ -451,22 +455,9 @@ int km_sum_x(km_ctx* c, double* out) {
   return KM_OK;
 }
 
-int km_sq_dev(km_ctx* c, const double* mu, double* out_local) {
-  KM_REQUIRE(c && c->loaded && mu && out_local, KM_ERR_STATE, "km_sq_dev: no data");
-  KM_HIP(hipSetDevice(c->device));
-  KM_HIP(hipMemcpyAsync(c->mu, mu, sizeof(double) * c->g.d, hipMemcpyHostToDevice, c->stream));
-  KM_HIP(hipMemsetAsync(c->moments, 0, sizeof(double), c->stream));
-  KM_HIP(km::launch_sq_dev(c->X, c->g, c->mu, c->moments, c->stream));
-  KM_HIP(hipMemcpyAsync(out_local, c->moments, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  KM_HIP(hipStreamSynchronize(c->stream));
-  return KM_OK;
-}
-
-int km_set_sse_base(km_ctx* c, double v) {
-  KM_REQUIRE(c && c->loaded, KM_ERR_STATE, "km_set_sse_base: no data");
-  KM_HIP(hipSetDevice(c->device));
-  KM_HIP(hipMemcpyAsync(c->sse_base, &v, sizeof(double), hipMemcpyHostToDevice, c->stream));
-  KM_HIP(hipStreamSynchronize(c->stream));
+int km_set_sse(km_ctx* c, int32_t enable) {
+  KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
+  c->want_sse = enable != 0;
   return KM_OK;
 }
 
@@ -488,6 +479,7 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
     KM_HIP(hipMalloc(&c->C64_cur, sizeof(double) * k * d));
     KM_HIP(hipMalloc(&c->C64_new, sizeof(double) * k * d));
     KM_HIP(hipMalloc(&c->C64T, sizeof(double) * k * d));
+    KM_HIP(hipMalloc(&c->C64P, sizeof(double) * kp * dp));
     KM_HIP(hipMalloc(&c->C32, sizeof(float) * kp * dp));
     KM_HIP(hipMalloc(&c->Chi, sizeof(_Float16) * kp * dp));
     KM_HIP(hipMalloc(&c->Clo, sizeof(_Float16) * kp * dp));
@@ -498,7 +490,7 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
     KM_HIP(hipMalloc(&c->bnd, sizeof(float) * 4));
     KM_HIP(hipMalloc(&c->cmax, sizeof(float)));
     KM_HIP(hipMalloc(&c->cabs, sizeof(float)));
-    KM_HIP(hipMalloc(&c->stats_own, sizeof(double) * (size_t)k * (d + 1)));
+    KM_HIP(hipMalloc(&c->stats_own, sizeof(double) * stats_len(c->g)));
     KM_HIP(hipMalloc(&c->work, sizeof(double) * 3 * k));
     KM_HIP(hipMalloc(&c->counts_dev, sizeof(int64_t) * k));
     KM_HIP(hipMalloc(&c->status_dev, sizeof(km::DevStatus)));
@@ -542,7 +534,7 @@ int km_assign_stats(km_ctx* c) {
 int km_stats_buffer(km_ctx* c, void** p, int64_t* len) {
   KM_REQUIRE(c && c->have_c && p && len, KM_ERR_STATE, "km_stats_buffer: set centroids first");
   *p = c->stats;
-  *len = (int64_t)c->g.k * (c->g.d + 1);
+  *len = (int64_t)stats_len(c->g);
   return KM_OK;
 }
 
@@ -557,8 +549,8 @@ int km_update(km_ctx* c, km_status* st, int64_t* counts) {
   KM_HIP(hipSetDevice(c->device));
   {
     ProfScope ps(c, KM_K_UPDATE);
-    KM_HIP(km::launch_update(c->stats, c->C64_cur, c->mu, c->g, c->C64_new, c->work, c->counts_dev, c->sse_base,
-                             c->qcount, c->ql.nwaves, c->status_dev, c->stream));
+    KM_HIP(km::launch_update(c->stats, c->C64_cur, c->g, c->C64_new, c->work, c->counts_dev, c->qcount,
+                             c->ql.nwaves, c->status_dev, c->stream));
   }
   KM_HIP(hipMemcpyAsync(c->status_host, c->status_dev, sizeof(km::DevStatus), hipMemcpyDeviceToHost, c->stream));
   KM_HIP(hipMemcpyAsync(c->counts_host, c->counts_dev, sizeof(int64_t) * c->g.k, hipMemcpyDeviceToHost, c->stream));

@@ -93,14 +93,10 @@ class HipEngine:
         self._c(self.lib.km_sum_x(self.ctx, _ptr(out, _PD)), "km_sum_x")
         return out
 
-    def sq_dev(self, mu: np.ndarray) -> float:
-        mu = np.ascontiguousarray(mu, dtype=np.float64)
-        out = np.zeros(1, dtype=np.float64)
-        self._c(self.lib.km_sq_dev(self.ctx, _ptr(mu, _PD), _ptr(out, _PD)), "km_sq_dev")
-        return float(out[0])
-
-    def set_sse_base(self, v: float) -> None:
-        self._c(self.lib.km_set_sse_base(self.ctx, float(v)), "km_set_sse_base")
+    def set_sse(self, enable: bool) -> None:
+        """compute_sse: residuals of every row summed into the stats buffer's
+        SSE slot during assign_stats (kmeans_spark.py:278-286)."""
+        self._c(self.lib.km_set_sse(self.ctx, 1 if enable else 0), "km_set_sse")
 
     # -- centroids / iteration -------------------------------------------------
     def set_centroids(self, C: np.ndarray) -> None:
@@ -109,7 +105,7 @@ class HipEngine:
         self._c(self.lib.km_set_centroids(self.ctx, _ptr(C, _PD), k, d), "km_set_centroids")
         if self.distributed and (self._stats_t is None or k != self.k):
             torch = self._torch
-            self._stats_t = torch.zeros(k * (d + 1), dtype=torch.float64, device=f"cuda:{self.device}")
+            self._stats_t = torch.zeros(k * (d + 1) + 1, dtype=torch.float64, device=f"cuda:{self.device}")
             torch.cuda.synchronize(self.device)
             self._c(self.lib.km_bind_stats_buffer(self.ctx, ctypes.c_void_p(self._stats_t.data_ptr())),
                     "km_bind_stats_buffer")

@@ -10,7 +10,7 @@ reference; the Lloyd iteration itself runs on the GPU (``engine.HipEngine``):
   mapPartitions(assign_partition)  L161-171   km_assign_stats (screen + exact resolve + stats)
   reduceByKey(..).collect()        L169-173   one RCCL all-reduce of the [k][d+1] stats
   _update_centroids                L176-206   km_update (+ host empty-cluster repair)
-  _compute_sse                     L208-237   closed form from the same statistics
+  _compute_sse                     L208-237   float64 residual of every row, same pass (SSE slot)
   NaN check / shift / log / commit L289-313   identical, from the device status
 
 There is no CPU fallback: without the HIP extension or a gfx950 GPU, ``fit``
@@ -51,11 +51,6 @@ class LloydRunner:
             self.engine.load_blobs(pl.n_local, b.d, pl.row0, b.n_centers, b.box, b.std, b.seed)
         else:
             self.engine.load_host(pl.local_rows)
-        # data moments for the closed-form SSE (float64, global)
-        s = self.comm.allreduce_np(self.engine.sum_x())
-        mu = s / max(pl.n_global, 1)
-        a = self.comm.allreduce_np(np.array([self.engine.sq_dev(mu)]))[0]
-        self.engine.set_sse_base(a)
 
     def rows(self, gidx: List[int]) -> np.ndarray:
         """Rows by global index (what ``rdd.takeSample`` returns, L72/L196)."""
@@ -225,6 +220,7 @@ class KMeans:
             say(f"SSE computation: {'ENABLED' if self.compute_sse else 'DISABLED (for performance)'}")
         out_dtype = run.pl.dtype
         run.engine.set_centroids(np.asarray(self.centroids, dtype=np.float64))
+        run.engine.set_sse(self.compute_sse)
         try:
             for iteration in range(self.max_iter):             # L266
                 if run.iteration(self, iteration, say):

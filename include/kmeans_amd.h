@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KM_ABI_VERSION 1
+#define KM_ABI_VERSION 2
 
 #define KM_OK 0
 #define KM_EMPTY 1          /* informational: the update found empty clusters */
@@ -95,12 +95,12 @@ int km_load_rows(km_ctx* ctx, int64_t row0, const float* rows, int64_t nrows);
 /* Synthetic Gaussian blobs generated in HBM, keyed by global row (benchmarks). */
 int km_generate_blobs(km_ctx* ctx, int64_t n, int32_t d, int64_t global_row0, int32_t n_centers, float box,
                       float stddev, uint64_t seed);
-/* Data moments for the SSE closed form: local sum_p x_p (float64 [d]); then,
- * given the global mean mu, the local sum_p ||x_p - mu||^2; then the global
- * value of that sum (all-reduced by the caller). */
+/* Local sum_p x_p of the resident rows (float64 [d]; integrity checks). */
 int km_sum_x(km_ctx* ctx, double* out_d);
-int km_sq_dev(km_ctx* ctx, const double* mu, double* out_local);
-int km_set_sse_base(km_ctx* ctx, double global_sq_dev);
+/* compute_sse (kmeans_spark.py:38, 278-286): when enabled, km_assign_stats
+ * also adds every row's float64 residual ||x - c_label||^2 to the SSE slot of
+ * the stats buffer (replaces _compute_sse's second pass, :208-237). */
+int km_set_sse(km_ctx* ctx, int32_t enable);
 
 /* Set the current centroids: replaces sc.broadcast(self.centroids)
  * (kmeans_spark.py:268, 340). */
@@ -111,17 +111,19 @@ int km_get_centroids(km_ctx* ctx, int32_t which, double* out);
 /* Assignment + partial statistics of one iteration: replaces
  * rdd.mapPartitions(assign_partition) + the map-side combine of
  * reduceByKey (kmeans_spark.py:147-171).  Output = the stats buffer
- * (float64 [k][d+1]: per-cluster sum of x, then count). */
+ * (float64 [k][d+1]: per-cluster sum of x, then count; then one SSE slot,
+ * 0 unless km_set_sse is on). */
 int km_assign_stats(km_ctx* ctx);
-/* The stats buffer (device) and its length in doubles; a caller may bind an
- * external device buffer instead (e.g. a torch tensor it all-reduces):
- * this is the reduceByKey shuffle + collect (kmeans_spark.py:169-173). */
+/* The stats buffer (device) and its length in doubles, k (d+1) + 1; a caller
+ * may bind an external device buffer instead (e.g. a torch tensor it
+ * all-reduces): this is the reduceByKey shuffle + collect
+ * (kmeans_spark.py:169-173) and the partition-SSE .sum() (:237). */
 int km_stats_buffer(km_ctx* ctx, void** dev_ptr, int64_t* len);
 int km_bind_stats_buffer(km_ctx* ctx, void* dev_ptr);
 
 /* Centroid update from the (all-reduced) stats: replaces _update_centroids
- * (kmeans_spark.py:176-206), the SSE pass (:208-237, closed form) and the
- * shift computation (:293-294).  Synchronises; fills *st and counts[k].
+ * (kmeans_spark.py:176-206), reads the SSE slot (:208-237) and computes the
+ * shifts (:293-294).  Synchronises; fills *st and counts[k].
  * Returns KM_EMPTY when clusters are empty (their new centroid is the old
  * one until km_replace_rows). */
 int km_update(km_ctx* ctx, km_status* st, int64_t* counts);

@@ -4,8 +4,9 @@ Used by the ``-m "not gpu"`` tests to exercise the product's host logic
 (KMeans driver, data placement, takeSample policy, empty-cluster repair,
 logging, the multi-rank all-reduce path over ``gloo``) without a GPU.  It is
 injected through ``KMeans._engine_factory``; the product never imports it.
-Arithmetic mirrors the device path: float32 rows, float64 statistics,
-closed-form SSE.
+Arithmetic mirrors the device path: float32 rows, float64 statistics, the
+SSE as the sum of every row's float64 residual to its pre-update centroid
+(an extra slot of the all-reduced statistics buffer).
 """
 import numpy as np
 
@@ -21,8 +22,7 @@ class OracleEngine:
     def __init__(self, comm):
         self.distributed = comm.world > 1
         self.n = self.d = self.k = 0
-        self.mu = None
-        self.A = 0.0
+        self.sse = False
         self._stats_t = None
 
     # data -------------------------------------------------------------------
@@ -34,12 +34,8 @@ class OracleEngine:
     def sum_x(self):
         return self.X.sum(axis=0) if self.n else np.zeros(self.d)
 
-    def sq_dev(self, mu):
-        self.mu = np.asarray(mu, dtype=np.float64)
-        return float(((self.X - self.mu) ** 2).sum()) if self.n else 0.0
-
-    def set_sse_base(self, v):
-        self.A = float(v)
+    def set_sse(self, enable):
+        self.sse = bool(enable)
 
     # iteration --------------------------------------------------------------------
     def set_centroids(self, C):
@@ -52,29 +48,30 @@ class OracleEngine:
 
     def assign_stats(self):
         import torch
-        S = np.zeros((self.k, self.d + 1))
+        S = np.zeros(self.k * (self.d + 1) + 1)
+        T = S[:-1].reshape(self.k, self.d + 1)
         if self.n:
             self._labels = orc.assign(self.X, self.cur)[0]
-            np.add.at(S[:, :self.d], self._labels, self.X)
-            np.add.at(S[:, self.d], self._labels, 1.0)
+            np.add.at(T[:, :self.d], self._labels, self.X)
+            np.add.at(T[:, self.d], self._labels, 1.0)
+            if self.sse:
+                S[-1] = float(((self.X - self.cur[self._labels]) ** 2).sum())
         else:
             self._labels = np.zeros(0, dtype=np.int64)
-        self._stats_t = torch.from_numpy(S.ravel().copy())
+        self._stats_t = torch.from_numpy(S)
 
     def run_collective(self, fn):
         fn(self._stats_t)
 
     def update(self):
-        S = self._stats_t.numpy().reshape(self.k, self.d + 1)
+        flat = self._stats_t.numpy()
+        S = flat[:-1].reshape(self.k, self.d + 1)
         cnt = S[:, self.d]
         old = self.cur
         new = np.where(cnt[:, None] > 0, S[:, :self.d] / np.where(cnt > 0, cnt, 1)[:, None], old)
         self.new = new
         shift = np.sqrt(((new - old) ** 2).sum(axis=1))
-        cmu = old - self.mu
-        t = np.where(cnt > 0, -2.0 * (cmu * (S[:, :self.d] - cnt[:, None] * self.mu)).sum(1)
-                     + cnt * (cmu ** 2).sum(1), 0.0)
-        st = _Status(sse=self.A + float(t.sum()), max_shift=float(shift.max()), n_empty=int((cnt == 0).sum()),
+        st = _Status(sse=float(flat[-1]), max_shift=float(shift.max()), n_empty=int((cnt == 0).sum()),
                      nonfinite=int(not np.all(np.isfinite(new))), q_rerank=0, q_full=0)
         return st, cnt.astype(np.int64)
 

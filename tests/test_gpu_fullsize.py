@@ -42,6 +42,7 @@ def test_full_size_properties(N, d, k, centers, sample, chunk):
     eng = run.engine
     C0 = km._initialize_centroids(run)
     eng.set_centroids(C0)
+    eng.set_sse(True)
     sx = eng.sum_x()
 
     eng.assign_stats()
@@ -67,3 +68,8 @@ def test_full_size_properties(N, d, k, centers, sample, chunk):
     lab_ref, _, _ = orc.assign(np.asarray(Xs, dtype=np.float64), C0, chunk=chunk)
     np.testing.assert_array_equal(labels[gidx], lab_ref)
     assert np.isfinite(st.sse) and st.sse > 0
+    # the sampled rows' own residuals (float64, oracle distances) scaled to N
+    # bracket the SSE loosely: blobs of std 1, so ~d per row
+    _, mind, _ = orc.assign(np.asarray(Xs, dtype=np.float64), C0, chunk=chunk)
+    est = float(np.sum(mind ** 2)) * N / sample
+    assert 0.8 * est < st.sse < 1.25 * est, (st.sse, est)

@@ -94,11 +94,12 @@ def test_takesample_init_policy_matches_reference(golden, name):
     np.testing.assert_array_equal(labels, g["labels"])
 
 
-def _blobs(n, d, centers, seed):
+def _blobs(n, d, centers, seed, box=10.0, std=1.0, with_labels=False):
     rng = np.random.default_rng(seed)
-    C = rng.uniform(-10, 10, (centers, d))
-    X = C[rng.integers(0, centers, n)] + rng.standard_normal((n, d))
-    return X.astype(np.float32).astype(np.float64)
+    C = rng.uniform(-box, box, (centers, d))
+    lab = rng.integers(0, centers, n)
+    X = (C[lab] + std * rng.standard_normal((n, d))).astype(np.float32).astype(np.float64)
+    return (X, lab) if with_labels else X
 
 
 def _one_step(X, C0, compute_sse=True, iters=1):
@@ -211,3 +212,27 @@ def test_near_ties_one_ulp_apart_vs_oracle(n, d, nb, off):
     labels = _one_step(X, C0, iters=1)._runner.engine.labels()
     lab_ref = orc.assign(X, C0)[0]
     np.testing.assert_array_equal(labels, lab_ref)
+
+
+@pytest.mark.parametrize("n,d,k,centers", [
+    (20000, 16, 8, 8),          # c2 shape: small path, residuals fused in k_assign_small
+    (20000, 64, 256, 256),      # c3 shape: fused kernel, residuals in the k_sse pass
+    (12000, 32, 1024, 256),     # c4 shape: unfused MFMA path, k_stats + k_sse
+    (12000, 128, 4096, 512),    # c5 shape: label-sorted statistics, residuals fused in k_segsum
+    (5000, 64, 300, 60),        # unfused, LDS-range statistics + k_sse
+])
+def test_tight_clusters_sse_vs_oracle(n, d, k, centers):
+    # std 1e-3 in a +-1000 box: sum ||x||^2 is ~1e12 x the SSE.  The reference
+    # sums min(norm)**2 per point (kmeans_spark.py:224-237); a closed form
+    # through ||x||^2 loses ~1e-5 relative here (north-star bar 1e-6)
+    X, blob = _blobs(n, d, centers, seed=7 + d, box=1000.0, std=1e-3, with_labels=True)
+    first = [int(np.nonzero(blob == b)[0][0]) for b in range(centers)]
+    rest = np.setdiff1d(np.arange(n), first)
+    extra = np.random.default_rng(3).choice(rest, k - centers, replace=False) if k > centers else []
+    C0 = X[np.concatenate([first, extra]).astype(np.int64)]
+    km = _one_step(X, C0)
+    ref = orc.lloyd_fit(X, k, 1, 1e-12, 0, True, 1, init_centroids=C0)
+    assert ref["sse_history"][0] < 1e-4 * np.sum(X * X)   # the regime that cancels
+    np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)
+    if not ref["records"][0]["empty"]:
+        np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)

@@ -15,6 +15,7 @@ from conftest import ROOT
 from oracle import kmeans_oracle as orc
 
 HEADER = os.path.join(ROOT, "include", "kmeans_amd.h")
+INJECTED = ("empty", "ties", "tight", "tight_wide")  # golden cases that inject their initial centroids
 
 
 def _ka():
@@ -32,7 +33,21 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert declared == set(_lib.exported_symbols()), declared ^ set(_lib.exported_symbols())
-    assert lib.km_abi_version() == 1
+    assert lib.km_abi_version() == 2
+
+
+def test_product_library_has_no_diagnostic_kernels():
+    # the ablation variants (results wrong by design) and the environment
+    # knobs exist only in the diagnostic build (make diag, -DKM_DIAG)
+    import subprocess
+    from kmeans_amd import _lib
+    syms = subprocess.run(["nm", "-C", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    fused = re.findall(r"k_fused<\d+, \d+, (?:true|false), (\d+)>", syms)
+    mfma = re.findall(r"k_assign_mfma<\d+, \d+, (\d+), (?:true|false)>", syms)
+    assert fused and mfma, "kernel symbols not found"
+    assert set(fused) == {"0"} and set(mfma) == {"0"}, (set(fused), set(mfma))
+    assert "getenv" not in subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True,
+                                          text=True, check=True).stdout
 
 
 def test_no_cpu_fallback_without_gpu():
@@ -143,11 +158,11 @@ def _fit(g, inject=True):
     return km, buf.getvalue(), np.array(km.predict(rdd, sc).collect())
 
 
-@pytest.mark.parametrize("name", ["test_a", "test_d", "empty", "ties", "test_c"])
+@pytest.mark.parametrize("name", ["test_a", "test_d", "empty", "ties", "test_c", "tight", "tight_wide"])
 def test_driver_reproduces_reference_with_cpu_engine(golden, cpu_engine, name):
     from test_gpu_parity import assert_logs_match
     g = golden(name)
-    km, out, labels = _fit(g, inject=(name in ("empty", "ties")))
+    km, out, labels = _fit(g, inject=(name in INJECTED))
     np.testing.assert_allclose(km.centroids, g["centroids"], rtol=1e-9, atol=1e-9)
     np.testing.assert_allclose(km.sse_history, g["sse_history"], rtol=1e-9)
     assert_logs_match(out, g["stdout"])
@@ -178,7 +193,7 @@ def _rank_main(rank, world, port, name, q):
         from conftest import load_golden
         ka.KMeans._engine_factory = staticmethod(ce.factory)
         g = load_golden(name)
-        km, out, labels = _fit(g, inject=(name in ("empty", "ties")))
+        km, out, labels = _fit(g, inject=(name in INJECTED))
         q.put((rank, km.centroids, km.sse_history, labels, out))
     finally:
         dist.destroy_process_group()
