@@ -92,9 +92,12 @@ def _pin_runtime():
         pass
 
 
-def load(path: str = LIB_PATH):
-    """Load (once) and return the ctypes library; raises RuntimeError if absent."""
+def load(path: str = None):
+    """Load (once) and return the ctypes library; raises RuntimeError if absent.
+    ``path`` defaults to ``LIB_PATH`` as it is at the first call (diagnostic
+    scripts point it at libkmeans_amd_diag.so before anything loads)."""
     global _lib
+    path = path or LIB_PATH
     with _lock:
         if _lib is not None:
             return _lib

@@ -1,6 +1,8 @@
 """c2 small path: assign kernel with fused float64 statistics (Lloyd step) vs
 the same kernel without them (predict), HIP-event averages.  Shows how much of
-k_assign_small is the LDS statistics table.  Usage: python scripts/small_probe.py [config] [N]"""
+k_assign_small is the LDS statistics table.
+Usage: python scripts/small_probe.py [config] [N] [--diag]   (--diag: load the
+diagnostic library, libkmeans_amd_diag.so, whose KM_* environment knobs apply)"""
 import os
 import sys
 
@@ -8,6 +10,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402  (CONFIGS, package alias)
 import kmeans_amd  # noqa: E402
+if "--diag" in sys.argv:
+    sys.argv.remove("--diag")
+    kmeans_amd._lib.LIB_PATH = kmeans_amd._lib.LIB_PATH.replace("libkmeans_amd.so", "libkmeans_amd_diag.so")
 from kmeans_amd.comm import Communicator  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
