@@ -26,9 +26,14 @@ KERNEL_KINDS = {"assign": KM_K_ASSIGN, "resolve": KM_K_RESOLVE, "stats": KM_K_ST
                 "prep": KM_K_PREP}
 
 
+KM_STOP_CONVERGED, KM_STOP_EMPTY, KM_STOP_NONFINITE = 1, 2, 3
+KM_MAX_BATCH = 32
+
+
 class KmStatus(ctypes.Structure):
     _fields_ = [("sse", ctypes.c_double), ("max_shift", ctypes.c_double), ("n_empty", ctypes.c_int32),
-                ("nonfinite", ctypes.c_int32), ("q_rerank", ctypes.c_int32), ("q_full", ctypes.c_int32)]
+                ("nonfinite", ctypes.c_int32), ("q_rerank", ctypes.c_int32), ("q_full", ctypes.c_int32),
+                ("ran", ctypes.c_int32), ("stop_reason", ctypes.c_int32)]
 
 
 class KmInfo(ctypes.Structure):
@@ -66,6 +71,9 @@ SIGNATURES = {
     "km_stats_buffer": [_P, ctypes.POINTER(_P), _PI64],
     "km_bind_stats_buffer": [_P, _P],
     "km_update": [_P, ctypes.POINTER(KmStatus), _PI64],
+    "km_batch_begin": [_P],
+    "km_update_async": [_P, _D],
+    "km_batch_end": [_P, ctypes.POINTER(KmStatus), _PI64, _PI32],
     "km_replace_rows": [_P, _PI32, _PD, _I32],
     "km_commit": [_P],
     "km_gather_rows": [_P, _PI64, _I32, _PD],

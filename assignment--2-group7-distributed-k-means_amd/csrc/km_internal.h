@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/kmeans_amd.h"
+
 namespace km {
 
 // Ambiguous-point queue entry written by the screening kernels and consumed
@@ -25,7 +27,10 @@ struct DevStatus {
   int32_t nonfinite;   // any non-finite new centroid (L289)
   int32_t q_rerank;    // screened points re-ranked exactly
   int32_t q_full;      // screened points that needed the full exact scan
+  int32_t ran;         // 0: the iteration was a no-op of a stopped batch
+  int32_t stop;        // KM_STOP_* raised by this iteration (batches)
 };
+static_assert(sizeof(DevStatus) == 40, "layout of km_status");
 
 // Per-wave segments of the ambiguous-point queue written by k_assign_mfma:
 // wave w owns entries [w*seg, w*seg + qcount[2w]); qcount[2w+1] = full scans.
@@ -46,11 +51,11 @@ struct Geometry {
 // C64P: float64 centroids padded to [kp][dp] (zero padding), the source of
 // the SSE residuals (aligned rows, no per-feature bound checks)
 hipError_t launch_prep_centroids(const double* C64, const Geometry& g, float* C32, float* cn2, float* cmax,
-                                 float* cabs, double* C64T, double* C64P, hipStream_t s);
+                                 float* cabs, double* C64T, double* C64P, const int* gate, hipStream_t s);
 // fp16 hi/lo split of -2*c*s and ||c||^2 s^2 for the MFMA screen (s from the
 // data and centroid abs maxima)
 hipError_t launch_prep_split(const float* C32, const Geometry& g, const float* cn2, const float* xabs,
-                             const float* cabs, _Float16* Chi, _Float16* Clo, float* cn2s, hipStream_t s);
+                             const float* cabs, _Float16* Chi, _Float16* Clo, float* cn2s, const int* gate, hipStream_t s);
 hipError_t launch_absmax(const float* X, int64_t nfloats, float* out, hipStream_t s);
 // Small k*d path: direct-form fp32 screening, in-thread exact re-rank,
 // optional fused statistics (LDS float64 table, replicated per lane).
@@ -58,14 +63,14 @@ hipError_t launch_absmax(const float* X, int64_t nfloats, float* out, hipStream_
 // stats[k (d+1)] (the SSE slot, kmeans_spark.py:224-237)
 hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C32, const double* C64,
                                const float* cmax, int32_t* labels, double* stats, int fuse_stats, int want_sse,
-                               int n_cu, hipStream_t s);
+                               int n_cu, const int* gate, hipStream_t s);
 bool small_path_ok(const Geometry& g);
 // MFMA path: fp16x3 screening on v_mfma_f32_32x32x16_f16, top-3 keys,
 // ambiguous points queued for the exact resolvers.
 hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16* Chi, const _Float16* Clo,
                               const float* cn2s, const float* cmax, const float* xabs, const float* cabs,
                               int32_t* labels, QEntry* queue, uint32_t* qcount, int n_cu, QLayout* ql,
-                              hipStream_t s);
+                              const int* gate, hipStream_t s);
 // queue capacity (entries) and per-wave counter words needed for n rows
 size_t queue_capacity(int64_t n, int n_cu);
 size_t qcount_words(int n_cu);
@@ -73,7 +78,7 @@ bool mfma_path_ok(const Geometry& g);
 // stats != nullptr: also add the resolved points' rows to the partial sums
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
-                          double* stats, int n_cu, hipStream_t s);
+                          double* stats, int n_cu, const int* gate, hipStream_t s);
 // Fused assign + partial sums (kp*dp <= 16384 class): fp16 hi image in VGPRs,
 // lo image + float64 sum table in LDS; decided points summed here, queued
 // points (and their counts) by launch_resolve(stats).
@@ -88,9 +93,9 @@ int diag_env(const char* name, int dflt);
 hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, const _Float16* Chi,
                         const _Float16* Clo, uint4* ChiF, uint4* CloF, const float* cn2s, const float* bnd,
                         const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,
-                        double* stats, int with_stats, int n_cu, QLayout* ql, hipStream_t s);
+                        double* stats, int with_stats, int n_cu, QLayout* ql, const int* gate, hipStream_t s);
 hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float* cabs, int dp, float* bnd,
-                               hipStream_t s);
+                               const int* gate, hipStream_t s);
 hipError_t launch_row_norm(const float* X, const Geometry& g, float* xnorm, hipStream_t s);
 // large k: counting sort of the labels + per-cluster float64 row sums (X read
 // once); scratch = sorted_stats_words(n, k) uint32 words
@@ -98,17 +103,19 @@ bool stats_needs_sort(const Geometry& g);
 size_t sorted_stats_words(int64_t n, int k);
 // C64P != nullptr: the SSE residuals are accumulated in the same pass
 hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t* labels, double* stats,
-                               uint32_t* scratch, const double* C64P, int n_cu, hipStream_t s);
+                               uint32_t* scratch, const double* C64P, int n_cu, const int* gate, hipStream_t s);
 hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels, double* stats, int n_cu,
-                        hipStream_t s);
+                        const int* gate, hipStream_t s);
 // SSE of the final labels (kmeans_spark.py:224-237): sum over rows of the
 // float64 residual ||x - c_label||^2, added to *sse (one atomic per wave)
 hipError_t launch_sse(const float* X, const Geometry& g, const int32_t* labels, const double* C64P, double* sse,
-                      hipStream_t s);
+                      const int* gate, hipStream_t s);
 // stats = [k][d+1] sums and counts, then the SSE slot stats[k (d+1)]
+// gate: the batch's stop flag (kernels of later iterations no-op once it is
+// set); stop_tol >= 0 lets k_finalize raise it (KM_STOP_*), < 0 never
 hipError_t launch_update(const double* stats, const double* C64_old, const Geometry& g, double* C64_new,
                          double* work, int64_t* counts, const uint32_t* qcount, uint32_t nq, DevStatus* status,
-                         hipStream_t s);
+                         int* gate, double stop_tol, hipStream_t s);
 hipError_t launch_sum_x(const float* X, const Geometry& g, double* out, hipStream_t s);
 hipError_t launch_gather_rows(const float* X, const Geometry& g, const int64_t* idx, int32_t n, double* out,
                               hipStream_t s);

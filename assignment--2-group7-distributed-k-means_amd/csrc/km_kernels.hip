@@ -90,7 +90,8 @@ __host__ __device__ inline float screen_b0(float xn_s, float cm_s, float pm_s, i
 __global__ __launch_bounds__(64) void k_prep_centroids(const double* __restrict__ C64, int k, int d, int dp,
                                                        float* __restrict__ C32, float* __restrict__ cn2,
                                                        float* __restrict__ cmax, float* __restrict__ cabs,
-                                                       double* __restrict__ C64T, double* __restrict__ C64P) {
+                                                       double* __restrict__ C64T, double* __restrict__ C64P, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   const int j = blockIdx.x;
   const int lane = threadIdx.x;
   double nn = 0.0;
@@ -120,14 +121,21 @@ __global__ __launch_bounds__(64) void k_prep_centroids(const double* __restrict_
   }
 }
 
+__global__ void k_zero_maxima(float* __restrict__ cmax, float* __restrict__ cabs, const int* __restrict__ gate) {
+  if (*gate) return;
+  if (threadIdx.x == 0) {
+    *cmax = 0.0f;
+    *cabs = 0.0f;
+  }
+}
+
 hipError_t launch_prep_centroids(const double* C64, const Geometry& g, float* C32, float* cn2, float* cmax,
-                                 float* cabs, double* C64T, double* C64P, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(cmax, 0, sizeof(float), s);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(cabs, 0, sizeof(float), s);
-  if (e != hipSuccess) return e;
+                                 float* cabs, double* C64T, double* C64P, const int* gate, hipStream_t s) {
+  // the two maxima are zeroed by a gated kernel (a memset would run in a
+  // stopped batch and leave the live images' bound inputs at zero)
+  hipLaunchKernelGGL(k_zero_maxima, dim3(1), dim3(64), 0, s, cmax, cabs, gate);
   hipLaunchKernelGGL(k_prep_centroids, dim3(g.kp), dim3(64), 0, s, C64, g.k, g.d, g.dp, C32, cn2, cmax, cabs, C64T,
-                     C64P);
+                     C64P, gate);
   return hipGetLastError();
 }
 
@@ -148,7 +156,8 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
                                                       const float* __restrict__ C32,
                                                       const double* __restrict__ C64,
                                                       const float* __restrict__ cmaxp, int32_t* __restrict__ labels,
-                                                      double* __restrict__ stats, int fuse, int want_sse, int R) {
+                                                      double* __restrict__ stats, int fuse, int want_sse, int R, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* sC = reinterpret_cast<float*>(smem);
   double* tab = reinterpret_cast<double*>(smem + ((k * DP * 4 + 15) / 16) * 16);
@@ -310,7 +319,7 @@ bool small_path_ok(const Geometry& g) {
 
 hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C32, const double* C64,
                                const float* cmax, int32_t* labels, double* stats, int fuse, int want_sse, int n_cu,
-                               hipStream_t s) {
+                               const int* gate, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
   const int R = small_replicas(g);
   const size_t lds = ((size_t)g.k * g.dp * 4 + 15) / 16 * 16 + (fuse ? (size_t)g.k * (g.d + 1) * 8 * R : 0);
@@ -321,19 +330,19 @@ hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C
   switch (g.dp) {
     case 16:
       hipLaunchKernelGGL(k_assign_small<16>, dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d, g.k, C32, C64,
-                         cmax, labels, stats, fuse, want_sse, R);
+                         cmax, labels, stats, fuse, want_sse, R, gate);
       break;
     case 32:
       hipLaunchKernelGGL(k_assign_small<32>, dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d, g.k, C32, C64,
-                         cmax, labels, stats, fuse, want_sse, R);
+                         cmax, labels, stats, fuse, want_sse, R, gate);
       break;
     case 48:
       hipLaunchKernelGGL(k_assign_small<48>, dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d, g.k, C32, C64,
-                         cmax, labels, stats, fuse, want_sse, R);
+                         cmax, labels, stats, fuse, want_sse, R, gate);
       break;
     case 64:
       hipLaunchKernelGGL(k_assign_small<64>, dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d, g.k, C32, C64,
-                         cmax, labels, stats, fuse, want_sse, R);
+                         cmax, labels, stats, fuse, want_sse, R, gate);
       break;
     default:
       return hipErrorInvalidValue;
@@ -373,7 +382,8 @@ __device__ __forceinline__ float mfma_scale(float xabs, float cabs) {
 __global__ __launch_bounds__(64) void k_prep_split(const float* __restrict__ C32, int kp, int dp,
                                                    const float* __restrict__ cn2, const float* __restrict__ xabs,
                                                    const float* __restrict__ cabs, _Float16* __restrict__ Chi,
-                                                   _Float16* __restrict__ Clo, float* __restrict__ cn2s, int k) {
+                                                   _Float16* __restrict__ Clo, float* __restrict__ cn2s, int k, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   const int j = blockIdx.x;
   const float s = mfma_scale(*xabs, *cabs);
   for (int f = threadIdx.x; f < dp; f += 64) {
@@ -419,6 +429,7 @@ struct MfmaArgs {
   int32_t* labels;
   QEntry* queue;
   uint32_t* qcount;
+  const int* gate;  // nonzero: a stopped batch, the launch is a no-op
 };
 
 // LDS image of a centroid chunk: for block b (32 centroids) and K-step t the
@@ -432,6 +443,7 @@ struct MfmaArgs {
 // whose best two share a chain then has no re-rank certificate (full scan).
 template <int NS, int WAVES, int ABL = 0, bool T2 = false>
 __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_assign_mfma(MfmaArgs A) {
+  if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   constexpr int DP = 16 * NS;
   constexpr int BLKB = NS * 1024;  // bytes of one block's fragments (one of hi / lo)
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -741,9 +753,9 @@ bool mfma_path_ok(const Geometry& g) {
 }
 
 hipError_t launch_prep_split(const float* C32, const Geometry& g, const float* cn2, const float* xabs,
-                             const float* cabs, _Float16* Chi, _Float16* Clo, float* cn2s, hipStream_t s) {
+                             const float* cabs, _Float16* Chi, _Float16* Clo, float* cn2s, const int* gate, hipStream_t s) {
   hipLaunchKernelGGL(k_prep_split, dim3(g.kp), dim3(64), 0, s, C32, g.kp, g.dp, cn2, xabs, cabs, Chi, Clo, cn2s,
-                     g.k);
+                     g.k, gate);
   return hipGetLastError();
 }
 
@@ -789,7 +801,7 @@ static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, con
 hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16* Chi, const _Float16* Clo,
                               const float* cn2s, const float* cmax, const float* xabs, const float* cabs,
                               int32_t* labels, QEntry* queue, uint32_t* qcount, int n_cu, QLayout* ql,
-                              hipStream_t s) {
+                              const int* gate, hipStream_t s) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
@@ -809,7 +821,7 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
   const uint32_t seg = (uint32_t)(((nwt + nb - 1) / nb) * 32);
   ql->seg = seg;
   ql->nwaves = (uint32_t)(nb * waves);
-  MfmaArgs a{X, g.n, g.k, g.kp, KC, seg, Chi, Clo, cn2s, cmax, xabs, cabs, labels, queue, qcount};
+  MfmaArgs a{X, g.n, g.k, g.kp, KC, seg, Chi, Clo, cn2s, cmax, xabs, cabs, labels, queue, qcount, gate};
   switch (g.dp / 16) {
     case 1: launch_mfma_ns<1>(waves, nb, lds, s, a); break;
     case 2: launch_mfma_ns<2>(waves, nb, lds, s, a); break;
@@ -907,6 +919,7 @@ struct FusedArgs {
   QEntry* queue;
   uint32_t* qcount;
   double* stats;       // [k][d+1] (sums, counts)
+  const int* gate;     // nonzero: a stopped batch, the launch is a no-op
 };
 
 constexpr int ceil_log2_c(int v) { return v <= 1 ? 0 : 1 + ceil_log2_c((v + 1) / 2); }
@@ -924,6 +937,7 @@ __device__ __forceinline__ void perm_halves(uint32_t v, uint32_t& lo, uint32_t& 
 // 7 = full kernel with s_memtime phase stamps, 8 = full kernel, compiler schedule
 template <int NS, int NB, bool STATS, int ABL = 0>
 __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
+  if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   constexpr int DP = 16 * NS;
   constexpr int KP = 32 * NB;
   constexpr int WAVES = 4;
@@ -1289,7 +1303,8 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
 // 8 halves of row 32 b + (l & 31), features 16 t + 8 (l >> 5) .. + 8
 __global__ __launch_bounds__(256) void k_frag_images(const _Float16* __restrict__ Chi, const _Float16* __restrict__ Clo,
                                                      int kp, int dp, uint4* __restrict__ ChiF,
-                                                     uint4* __restrict__ CloF) {
+                                                     uint4* __restrict__ CloF, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   const int ns = dp / 16;
   const int total = (kp / 32) * ns * 64;
   const int id = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1304,7 +1319,8 @@ __global__ __launch_bounds__(256) void k_frag_images(const _Float16* __restrict_
 
 // screening-bound constants: B0 = alpha * ||x|| + beta (see k_assign_mfma)
 __global__ void k_bound_consts(const float* __restrict__ cmax, const float* __restrict__ xabs,
-                               const float* __restrict__ cabs, int dp, float* __restrict__ bnd) {
+                               const float* __restrict__ cabs, int dp, float* __restrict__ bnd, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   // screen_b0 is affine in xn_s = s ||x||: B0 = bnd[0] ||x|| + bnd[1]
   const float s = mfma_scale(*xabs, *cabs);
   const float cm = *cmax * s;
@@ -1389,14 +1405,14 @@ bool fused_path_ok(const Geometry& g) {
 hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, const _Float16* Chi,
                         const _Float16* Clo, uint4* ChiF, uint4* CloF, const float* cn2s, const float* bnd,
                         const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,
-                        double* stats, int with_stats, int n_cu, QLayout* ql, hipStream_t s) {
+                        double* stats, int with_stats, int n_cu, QLayout* ql, const int* gate, hipStream_t s) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
   const int ns = g.dp / 16, nb = g.kp / 32;
   {
     const int total = nb * ns * 64;
-    hipLaunchKernelGGL(k_frag_images, dim3((total + 255) / 256), dim3(256), 0, s, Chi, Clo, g.kp, g.dp, ChiF, CloF);
+    hipLaunchKernelGGL(k_frag_images, dim3((total + 255) / 256), dim3(256), 0, s, Chi, Clo, g.kp, g.dp, ChiF, CloF, gate);
   }
   constexpr int WAVES = 4;
   const int64_t ntiles = (g.n + 31) / 32;
@@ -1407,7 +1423,7 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
   const uint32_t seg = (uint32_t)(((ntiles + nw - 1) / nw) * 32);
   ql->seg = seg;
   ql->nwaves = (uint32_t)nw;
-  FusedArgs a{X, xnorm, g.n, g.k, g.d, seg, ChiF, CloF, cn2s, bnd, xabs, cabs, labels, queue, qcount, stats};
+  FusedArgs a{X, xnorm, g.n, g.k, g.d, seg, ChiF, CloF, cn2s, bnd, xabs, cabs, labels, queue, qcount, stats, gate};
   const size_t lds = (size_t)g.kp * 4 + (with_stats ? (size_t)(g.dp + 1) * g.kp * 8 : 0);
 #define KM_FUSED_CASE(NS_, NB_)                                                                        \
   case NS_ * 100 + NB_:                                                                                \
@@ -1448,8 +1464,8 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
 }
 
 hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float* cabs, int dp, float* bnd,
-                               hipStream_t s) {
-  hipLaunchKernelGGL(k_bound_consts, dim3(1), dim3(1), 0, s, cmax, xabs, cabs, dp, bnd);
+                               const int* gate, hipStream_t s) {
+  hipLaunchKernelGGL(k_bound_consts, dim3(1), dim3(1), 0, s, cmax, xabs, cabs, dp, bnd, gate);
   return hipGetLastError();
 }
 
@@ -1539,7 +1555,8 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
                                                   const double* __restrict__ C64, const QEntry* __restrict__ queue,
                                                   const uint32_t* __restrict__ qcount, QLayout ql,
                                                   int32_t* __restrict__ labels, double* __restrict__ stats,
-                                                  int tab_kp) {
+                                                  int tab_kp, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* tab = reinterpret_cast<double*>(smem);
   uint32_t* pre = reinterpret_cast<uint32_t*>(smem + (stats && tab_kp ? (size_t)(d + 1) * tab_kp * 8 : 0));
@@ -1653,7 +1670,8 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
                                                    const double* __restrict__ C64T, const QEntry* __restrict__ queue,
                                                    const uint32_t* __restrict__ qcount, QLayout ql,
                                                    int32_t* __restrict__ labels, int ch,
-                                                   double* __restrict__ stats, int use_chain, int pair_chain) {
+                                                   double* __restrict__ stats, int use_chain, int pair_chain, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sCT = reinterpret_cast<double*>(smem);                                    // [d][ch]
   float* xs_all = reinterpret_cast<float*>(smem + (size_t)d * ch * 8);              // [8][G][d]
@@ -1812,7 +1830,7 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
 
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
-                          double* stats, int n_cu, hipStream_t s) {
+                          double* stats, int n_cu, const int* gate, hipStream_t s) {
   if (g.n == 0 || ql.nwaves == 0) return hipSuccess;
   constexpr size_t LDS_MAX = 160 * 1024;
   const size_t pre_bytes = ((size_t)ql.nwaves + 1) * 4;
@@ -1830,17 +1848,17 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   static const int fs_wg = diag_env("KM_FS_WG", 1);  // workgroups per CU (3: no measurable change)
   if (G == 4)
     hipLaunchKernelGGL(k_fullscan<4>, dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T, queue,
-                       qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain);
+                       qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, gate);
   else
     hipLaunchKernelGGL(k_fullscan<2>, dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T, queue,
-                       qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain);
+                       qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, gate);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t tab_bytes = (size_t)(g.d + 1) * g.kp * 8;
   const size_t pres = (stats ? 2 : 1) * pre_bytes;
   const int tab_kp = (stats && tab_bytes + pres <= LDS_MAX) ? g.kp : 0;
   hipLaunchKernelGGL(k_rerank2, dim3(n_cu), dim3(1024), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d, g.k,
-                     C64, queue, qcount, ql, labels, stats, tab_kp);
+                     C64, queue, qcount, ql, labels, stats, tab_kp, gate);
   return hipGetLastError();
 }
 
@@ -1859,7 +1877,8 @@ static constexpr int STATS_LDS = 156 * 1024;
 // k (d+1) doubles exceed LDS but k (fr+1) fit (c4: 1024 clusters x 16 features).
 __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int64_t n, int d, int dp, int k,
                                                 const int32_t* __restrict__ labels, double* __restrict__ stats,
-                                                int kr, int fr, int64_t rows_per_block) {
+                                                int kr, int fr, int64_t rows_per_block, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* tab = reinterpret_cast<double*>(smem);
   // LDS row of a cluster: fr feature slots + count.  Feature f0 + 4m + c is
@@ -1948,7 +1967,7 @@ static void stats_ranges(const Geometry& g, int* fr_out, int* kr_out) {
 }
 
 hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels, double* stats, int n_cu,
-                        hipStream_t s) {
+                        const int* gate, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
   if (g.dp > 256 || g.dp % 4) return hipErrorInvalidValue;
   int fr = 0, kr = 0;
@@ -1967,7 +1986,7 @@ hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels
   int64_t rpb = (g.n + bx - 1) / bx;
   rpb = (rpb + 63) / 64 * 64;
   hipLaunchKernelGGL(k_stats, dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024), lds, s, X, g.n,
-                     g.d, g.dp, g.k, labels, stats, kr, fr, rpb);
+                     g.d, g.dp, g.k, labels, stats, kr, fr, rpb, gate);
   return hipGetLastError();
 }
 
@@ -1980,7 +1999,8 @@ hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels
 // as gathered whole rows.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_hist(const int32_t* __restrict__ labels, int64_t n, int k,
-                                               uint32_t* __restrict__ cnt) {
+                                               uint32_t* __restrict__ cnt, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
   for (int i = threadIdx.x; i < k; i += blockDim.x) hist[i] = 0u;
@@ -1996,7 +2016,8 @@ __global__ __launch_bounds__(1024) void k_hist(const int32_t* __restrict__ label
 
 // exclusive scan of cnt[k] into off[k] and cur[k] (scatter cursors); one block
 __global__ __launch_bounds__(1024) void k_scan(const uint32_t* __restrict__ cnt, int k, uint32_t* __restrict__ off,
-                                               uint32_t* __restrict__ cur) {
+                                               uint32_t* __restrict__ cur, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   __shared__ uint32_t wsum[16];
   const int t = threadIdx.x;
   const int chunk = (k + 1023) / 1024;
@@ -2025,7 +2046,8 @@ __global__ __launch_bounds__(1024) void k_scan(const uint32_t* __restrict__ cnt,
 
 __global__ __launch_bounds__(256) void k_scatter(const int32_t* __restrict__ labels, int64_t n, int k,
                                                  uint32_t* __restrict__ cur, uint32_t* __restrict__ perm,
-                                                 int32_t* __restrict__ slab) {
+                                                 int32_t* __restrict__ slab, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int l = labels[i];
     if ((unsigned)l < (unsigned)k) {
@@ -2050,7 +2072,8 @@ template <int L>  // lanes per row = dp / 4
 __global__ __launch_bounds__(256) void k_segsum(const float* __restrict__ X, int d, int64_t n,
                                                 const uint32_t* __restrict__ perm, const int32_t* __restrict__ slab,
                                                 double* __restrict__ stats, const double* __restrict__ C64P,
-                                                double* __restrict__ sse) {
+                                                double* __restrict__ sse, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   constexpr int P = 64 / L;  // rows per wave-instruction
   constexpr int U = 4;       // instructions in flight
   constexpr int DP = 4 * L;
@@ -2135,7 +2158,8 @@ __global__ __launch_bounds__(256) void k_segsum(const float* __restrict__ X, int
 template <int L>
 __global__ __launch_bounds__(256) void k_sse(const float* __restrict__ X, int64_t n,
                                              const int32_t* __restrict__ labels, const double* __restrict__ C64P,
-                                             double* __restrict__ sse) {
+                                             double* __restrict__ sse, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   constexpr int P = 64 / L;
   constexpr int U = 4;
   constexpr int DP = 4 * L;
@@ -2178,7 +2202,7 @@ __global__ __launch_bounds__(256) void k_sse(const float* __restrict__ X, int64_
 }
 
 hipError_t launch_sse(const float* X, const Geometry& g, const int32_t* labels, const double* C64P, double* sse,
-                      hipStream_t s) {
+                      const int* gate, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
   const int L = g.dp / 4;
   const int P = 64 / L;
@@ -2186,21 +2210,22 @@ hipError_t launch_sse(const float* X, const Geometry& g, const int32_t* labels, 
   if (blocks > 8192) blocks = 8192;
   const dim3 grid((unsigned)blocks), blk(256);
   switch (L) {
-    case 4: hipLaunchKernelGGL(k_sse<4>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
-    case 8: hipLaunchKernelGGL(k_sse<8>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
-    case 12: hipLaunchKernelGGL(k_sse<12>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
-    case 16: hipLaunchKernelGGL(k_sse<16>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
-    case 24: hipLaunchKernelGGL(k_sse<24>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
-    case 32: hipLaunchKernelGGL(k_sse<32>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
-    case 48: hipLaunchKernelGGL(k_sse<48>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
-    case 64: hipLaunchKernelGGL(k_sse<64>, grid, blk, 0, s, X, g.n, labels, C64P, sse); break;
+    case 4: hipLaunchKernelGGL(k_sse<4>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
+    case 8: hipLaunchKernelGGL(k_sse<8>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
+    case 12: hipLaunchKernelGGL(k_sse<12>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
+    case 16: hipLaunchKernelGGL(k_sse<16>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
+    case 24: hipLaunchKernelGGL(k_sse<24>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
+    case 32: hipLaunchKernelGGL(k_sse<32>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
+    case 48: hipLaunchKernelGGL(k_sse<48>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
+    case 64: hipLaunchKernelGGL(k_sse<64>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
 // counts of the histogram into the count column
-__global__ void k_put_counts(const uint32_t* __restrict__ cnt, int k, int d, double* __restrict__ stats) {
+__global__ void k_put_counts(const uint32_t* __restrict__ cnt, int k, int d, double* __restrict__ stats, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j < k) stats[(size_t)j * (d + 1) + d] = (double)cnt[j];
 }
@@ -2219,7 +2244,7 @@ bool stats_needs_sort(const Geometry& g) {
 }
 
 hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t* labels, double* stats,
-                               uint32_t* scratch, const double* C64P, int n_cu, hipStream_t s) {
+                               uint32_t* scratch, const double* C64P, int n_cu, const int* gate, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
   if (g.dp > 256) return hipErrorInvalidValue;
   uint32_t* cnt = scratch;
@@ -2232,27 +2257,27 @@ hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t*
   if (hb > n_cu * 2) hb = n_cu * 2;
   const size_t hist_lds = (size_t)g.k * 4;
   if (hist_lds > 64 * 1024) return hipErrorInvalidValue;  // k <= 16384
-  hipLaunchKernelGGL(k_hist, dim3((unsigned)hb), dim3(1024), hist_lds, s, labels, g.n, g.k, cnt);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, cnt, g.k, off, cur);
+  hipLaunchKernelGGL(k_hist, dim3((unsigned)hb), dim3(1024), hist_lds, s, labels, g.n, g.k, cnt, gate);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, cnt, g.k, off, cur, gate);
   int64_t sb = (g.n + 255) / 256;
   if (sb > n_cu * 16) sb = n_cu * 16;
   int32_t* slab = reinterpret_cast<int32_t*>(perm + g.n);
-  hipLaunchKernelGGL(k_scatter, dim3((unsigned)sb), dim3(256), 0, s, labels, g.n, g.k, cur, perm, slab);
-  hipLaunchKernelGGL(k_put_counts, dim3((g.k + 255) / 256), dim3(256), 0, s, cnt, g.k, g.d, stats);
+  hipLaunchKernelGGL(k_scatter, dim3((unsigned)sb), dim3(256), 0, s, labels, g.n, g.k, cur, perm, slab, gate);
+  hipLaunchKernelGGL(k_put_counts, dim3((g.k + 255) / 256), dim3(256), 0, s, cnt, g.k, g.d, stats, gate);
   // every label is in [0, k) (the assign kernels map non-finite rows to 0),
   // so all n sorted positions are written
   const int64_t nsorted = g.n;
   int64_t wb = (int64_t)n_cu * 8;
   const unsigned grid = (unsigned)wb;
   switch (g.dp / 4) {
-    case 4: hipLaunchKernelGGL(k_segsum<4>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
-    case 8: hipLaunchKernelGGL(k_segsum<8>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
-    case 12: hipLaunchKernelGGL(k_segsum<12>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
-    case 16: hipLaunchKernelGGL(k_segsum<16>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
-    case 24: hipLaunchKernelGGL(k_segsum<24>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
-    case 32: hipLaunchKernelGGL(k_segsum<32>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
-    case 48: hipLaunchKernelGGL(k_segsum<48>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
-    case 64: hipLaunchKernelGGL(k_segsum<64>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1)); break;
+    case 4: hipLaunchKernelGGL(k_segsum<4>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1), gate); break;
+    case 8: hipLaunchKernelGGL(k_segsum<8>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1), gate); break;
+    case 12: hipLaunchKernelGGL(k_segsum<12>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1), gate); break;
+    case 16: hipLaunchKernelGGL(k_segsum<16>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1), gate); break;
+    case 24: hipLaunchKernelGGL(k_segsum<24>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1), gate); break;
+    case 32: hipLaunchKernelGGL(k_segsum<32>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1), gate); break;
+    case 48: hipLaunchKernelGGL(k_segsum<48>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1), gate); break;
+    case 64: hipLaunchKernelGGL(k_segsum<64>, dim3(grid), dim3(256), 0, s, X, g.d, nsorted, perm, slab, stats, C64P, stats + (size_t)g.k * (g.d + 1), gate); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -2266,7 +2291,8 @@ hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t*
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_update(const double* __restrict__ stats, const double* __restrict__ old,
                                                int k, int d, double* __restrict__ out, double* __restrict__ work,
-                                               int64_t* __restrict__ counts) {
+                                               int64_t* __restrict__ counts, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   const int j = blockIdx.x;
   const int lane = threadIdx.x;
   const int d1 = d + 1;
@@ -2290,10 +2316,23 @@ __global__ __launch_bounds__(64) void k_update(const double* __restrict__ stats,
   }
 }
 
+// Per-iteration status into *st (one history slot per iteration of a batch,
+// km_update_async).  In a batch (stop_tol >= 0) the gate is raised, and the
+// remaining enqueued iterations become no-ops, when the iteration converged
+// (max_shift < tol, kmeans_spark.py:310), produced empty clusters (the host
+// repairs them, L191-204) or non-finite centroids (L289); a gated launch only
+// records that the iteration did not run.
 __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ work, const int64_t* __restrict__ counts,
                                                   int k, const double* __restrict__ sse,
                                                   const uint32_t* __restrict__ qcount, uint32_t nq,
-                                                  DevStatus* __restrict__ st) {
+                                                  DevStatus* __restrict__ st, int* __restrict__ gate, double stop_tol) {
+  if (*gate) {
+    if (threadIdx.x == 0) {
+      st->ran = 0;
+      st->stop = 0;
+    }
+    return;
+  }
   __shared__ double s_max[256];
   __shared__ int s_emp[256], s_nf[256], s_q[256], s_qf[256];
   double mx = 0.0;
@@ -2324,23 +2363,36 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ wor
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    st->max_shift = sqrt(s_max[0]);
+    const double ms = sqrt(s_max[0]);
+    st->max_shift = ms;
     st->sse = *sse;
     st->n_empty = s_emp[0];
     st->nonfinite = s_nf[0];
     st->q_full = s_qf[0];
     st->q_rerank = s_q[0];
+    st->ran = 1;
+    int stop = 0;
+    if (stop_tol >= 0.0) {
+      if (s_nf[0])
+        stop = KM_STOP_NONFINITE;
+      else if (s_emp[0])
+        stop = KM_STOP_EMPTY;
+      else if (ms < stop_tol)
+        stop = KM_STOP_CONVERGED;
+    }
+    st->stop = stop;
+    if (stop) *gate = stop;
   }
 }
 
 hipError_t launch_update(const double* stats, const double* C64_old, const Geometry& g, double* C64_new,
                          double* work, int64_t* counts, const uint32_t* qcount, uint32_t nq, DevStatus* status,
-                         hipStream_t s) {
-  hipLaunchKernelGGL(k_update, dim3(g.k), dim3(64), 0, s, stats, C64_old, g.k, g.d, C64_new, work, counts);
+                         int* gate, double stop_tol, hipStream_t s) {
+  hipLaunchKernelGGL(k_update, dim3(g.k), dim3(64), 0, s, stats, C64_old, g.k, g.d, C64_new, work, counts, gate);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, work, counts, g.k, stats + (size_t)g.k * (g.d + 1),
-                     qcount, nq, status);
+                     qcount, nq, status, gate, stop_tol);
   return hipGetLastError();
 }
 

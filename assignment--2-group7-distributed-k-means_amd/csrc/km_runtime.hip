@@ -110,6 +110,18 @@ struct km_ctx {
   km::DevStatus* status_dev = nullptr;
   km::DevStatus* status_host = nullptr;
   int64_t* counts_host = nullptr;
+  // batches of iterations without host syncs (km_batch_begin / km_update_async /
+  // km_batch_end): per-iteration history, the stop gate every iteration kernel
+  // checks, and the centroid buffers each slot read and wrote
+  int* gate = nullptr;                 // device: 0 run, KM_STOP_* = stopped
+  km::DevStatus* hist = nullptr;       // device [KM_MAX_BATCH]
+  km::DevStatus* hist_host = nullptr;  // pinned
+  int64_t* hist_counts = nullptr;      // device [KM_MAX_BATCH][k]
+  int64_t* hist_counts_host = nullptr; // pinned
+  bool in_batch = false;
+  int batch_n = 0;
+  double* slot_cur[KM_MAX_BATCH] = {};
+  double* slot_new[KM_MAX_BATCH] = {};
   // staging
   float* pinned = nullptr;
   size_t pinned_floats = 0;
@@ -173,6 +185,12 @@ void free_centroids(km_ctx* c) {
   dfree(c->status_dev);
   hfree(c->status_host);
   hfree(c->counts_host);
+  dfree(c->hist);
+  hfree(c->hist_host);
+  dfree(c->hist_counts);
+  hfree(c->hist_counts_host);
+  c->in_batch = false;
+  c->batch_n = 0;
   if (c->stats != nullptr && c->stats != c->stats_own) {
     // external buffer: keep binding only if the size is unchanged (caller re-binds otherwise)
   }
@@ -203,9 +221,10 @@ void free_data(km_ctx* c) {
 int prep(km_ctx* c, const double* src) {
   ProfScope ps(c, KM_K_PREP);
   c->prep_of = src;
-  KM_HIP(km::launch_prep_centroids(src, c->g, c->C32, c->cn2, c->cmax, c->cabs, c->C64T, c->C64P, c->stream));
-  KM_HIP(km::launch_prep_split(c->C32, c->g, c->cn2, c->xabs, c->cabs, c->Chi, c->Clo, c->cn2s, c->stream));
-  KM_HIP(km::launch_bound_consts(c->cmax, c->xabs, c->cabs, c->g.dp, c->bnd, c->stream));
+  KM_HIP(km::launch_prep_centroids(src, c->g, c->C32, c->cn2, c->cmax, c->cabs, c->C64T, c->C64P, c->gate,
+                                   c->stream));
+  KM_HIP(km::launch_prep_split(c->C32, c->g, c->cn2, c->xabs, c->cabs, c->Chi, c->Clo, c->cn2s, c->gate, c->stream));
+  KM_HIP(km::launch_bound_consts(c->cmax, c->xabs, c->cabs, c->g.dp, c->bnd, c->gate, c->stream));
   return KM_OK;
 }
 
@@ -234,7 +253,7 @@ int run_assign(km_ctx* c, bool with_stats) {
   if (c->path == 1) {
     ProfScope ps(c, KM_K_ASSIGN);
     KM_HIP(km::launch_assign_small(c->X, g, c->C32, c->C64_cur, c->cmax, c->labels, c->stats, with_stats ? 1 : 0,
-                                   sse ? 1 : 0, c->n_cu, c->stream));
+                                   sse ? 1 : 0, c->n_cu, c->gate, c->stream));
     return KM_OK;
   }
   if (c->fused) {
@@ -242,30 +261,30 @@ int run_assign(km_ctx* c, bool with_stats) {
       ProfScope ps(c, KM_K_ASSIGN);
       KM_HIP(km::launch_fused(c->X, c->xnorm, g, c->Chi, c->Clo, c->ChiF, c->CloF, c->cn2s, c->bnd, c->xabs, c->cabs,
                               c->labels, c->queue, c->qcount, c->stats, with_stats ? 1 : 0, c->n_cu, &c->ql,
-                              c->stream));
+                              c->gate, c->stream));
     }
     {
       ProfScope ps(c, KM_K_RESOLVE);
       KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels,
-                                with_stats ? c->stats : nullptr, c->n_cu, c->stream));
+                                with_stats ? c->stats : nullptr, c->n_cu, c->gate, c->stream));
     }
     if (sse) {
       // the fused kernel's LDS holds the sum table: the residuals are a
       // second pass over the final labels (only when compute_sse)
       ProfScope ps(c, KM_K_STATS);
-      KM_HIP(km::launch_sse(c->X, g, c->labels, c->C64P, sse_slot, c->stream));
+      KM_HIP(km::launch_sse(c->X, g, c->labels, c->C64P, sse_slot, c->gate, c->stream));
     }
     return KM_OK;  // counts are part of the fused and resolver statistics
   }
   {
     ProfScope ps(c, KM_K_ASSIGN);
     KM_HIP(km::launch_assign_mfma(c->X, g, c->Chi, c->Clo, c->cn2s, c->cmax, c->xabs, c->cabs, c->labels, c->queue,
-                                  c->qcount, c->n_cu, &c->ql, c->stream));
+                                  c->qcount, c->n_cu, &c->ql, c->gate, c->stream));
   }
   {
     ProfScope ps(c, KM_K_RESOLVE);
     KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels, nullptr, c->n_cu,
-                              c->stream));
+                              c->gate, c->stream));
   }
   if (with_stats) {
     ProfScope ps(c, KM_K_STATS);
@@ -277,10 +296,10 @@ int run_assign(km_ctx* c, bool with_stats) {
         c->sort_words = words;
       }
       KM_HIP(km::launch_stats_sorted(c->X, g, c->labels, c->stats, c->sort_scratch, sse ? c->C64P : nullptr,
-                                     c->n_cu, c->stream));
+                                     c->n_cu, c->gate, c->stream));
     } else {
-      KM_HIP(km::launch_stats(c->X, g, c->labels, c->stats, c->n_cu, c->stream));
-      if (sse) KM_HIP(km::launch_sse(c->X, g, c->labels, c->C64P, sse_slot, c->stream));
+      KM_HIP(km::launch_stats(c->X, g, c->labels, c->stats, c->n_cu, c->gate, c->stream));
+      if (sse) KM_HIP(km::launch_sse(c->X, g, c->labels, c->C64P, sse_slot, c->gate, c->stream));
     }
   }
   return KM_OK;
@@ -324,6 +343,13 @@ int km_create(int device, km_ctx** out) {
     return fail(KM_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
   }
   c->stream = c->own_stream;
+  e = hipMalloc(&c->gate, sizeof(int));
+  if (e == hipSuccess) e = hipMemset(c->gate, 0, sizeof(int));
+  if (e != hipSuccess) {
+    (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return fail(KM_ERR_HIP, std::string("km_create: ") + hipGetErrorString(e));
+  }
   *out = c;
   return KM_OK;
 }
@@ -341,6 +367,7 @@ int km_destroy(km_ctx* c) {
       (void)hipEventDestroy(p.second);
     }
   for (auto e : c->pool) (void)hipEventDestroy(e);
+  dfree(c->gate);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return KM_OK;
@@ -496,6 +523,10 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
     KM_HIP(hipMalloc(&c->status_dev, sizeof(km::DevStatus)));
     KM_HIP(hipHostMalloc(&c->status_host, sizeof(km::DevStatus), hipHostMallocDefault));
     KM_HIP(hipHostMalloc(&c->counts_host, sizeof(int64_t) * k, hipHostMallocDefault));
+    KM_HIP(hipMalloc(&c->hist, sizeof(km::DevStatus) * KM_MAX_BATCH));
+    KM_HIP(hipHostMalloc(&c->hist_host, sizeof(km::DevStatus) * KM_MAX_BATCH, hipHostMallocDefault));
+    KM_HIP(hipMalloc(&c->hist_counts, sizeof(int64_t) * (size_t)k * KM_MAX_BATCH));
+    KM_HIP(hipHostMalloc(&c->hist_counts_host, sizeof(int64_t) * (size_t)k * KM_MAX_BATCH, hipHostMallocDefault));
     c->stats = c->stats_own;
     c->k_alloc = k;
     if (km::small_path_ok(c->g))
@@ -546,11 +577,12 @@ int km_bind_stats_buffer(km_ctx* c, void* p) {
 
 int km_update(km_ctx* c, km_status* st, int64_t* counts) {
   KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_update: set centroids first");
+  KM_REQUIRE(!c->in_batch, KM_ERR_STATE, "km_update: inside a batch (use km_update_async)");
   KM_HIP(hipSetDevice(c->device));
   {
     ProfScope ps(c, KM_K_UPDATE);
     KM_HIP(km::launch_update(c->stats, c->C64_cur, c->g, c->C64_new, c->work, c->counts_dev, c->qcount,
-                             c->ql.nwaves, c->status_dev, c->stream));
+                             c->ql.nwaves, c->status_dev, c->gate, -1.0, c->stream));
   }
   KM_HIP(hipMemcpyAsync(c->status_host, c->status_dev, sizeof(km::DevStatus), hipMemcpyDeviceToHost, c->stream));
   KM_HIP(hipMemcpyAsync(c->counts_host, c->counts_dev, sizeof(int64_t) * c->g.k, hipMemcpyDeviceToHost, c->stream));
@@ -569,9 +601,93 @@ int km_update(km_ctx* c, km_status* st, int64_t* counts) {
     st->nonfinite = s.nonfinite;
     st->q_rerank = s.q_rerank;
     st->q_full = s.q_full;
+    st->ran = s.ran;
+    st->stop_reason = s.stop;
   }
   if (counts) memcpy(counts, c->counts_host, sizeof(int64_t) * c->g.k);
   return s.n_empty > 0 ? KM_EMPTY : KM_OK;
+}
+
+int km_batch_begin(km_ctx* c) {
+  KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_batch_begin: set centroids first");
+  KM_REQUIRE(!c->in_batch, KM_ERR_STATE, "km_batch_begin: a batch is open");
+  KM_HIP(hipSetDevice(c->device));
+  KM_HIP(hipMemsetAsync(c->gate, 0, sizeof(int), c->stream));
+  c->in_batch = true;
+  c->batch_n = 0;
+  return KM_OK;
+}
+
+int km_update_async(km_ctx* c, double tol) {
+  KM_REQUIRE(c && c->have_c && c->in_batch, KM_ERR_STATE, "km_update_async: call km_batch_begin first");
+  KM_REQUIRE(c->batch_n < KM_MAX_BATCH, KM_ERR_ARG, "km_update_async: more than KM_MAX_BATCH iterations in a batch");
+  KM_REQUIRE(tol >= 0.0, KM_ERR_ARG, "km_update_async: tolerance must be >= 0");
+  KM_HIP(hipSetDevice(c->device));
+  const int slot = c->batch_n;
+  {
+    ProfScope ps(c, KM_K_UPDATE);
+    KM_HIP(km::launch_update(c->stats, c->C64_cur, c->g, c->C64_new, c->work,
+                             c->hist_counts + (size_t)slot * c->g.k, c->qcount, c->ql.nwaves, c->hist + slot,
+                             c->gate, tol, c->stream));
+  }
+  c->slot_cur[slot] = c->C64_cur;
+  c->slot_new[slot] = c->C64_new;
+  // speculative commit (kmeans_spark.py:307): the next iteration reads the
+  // new centroids; a stopped batch's later kernels (prep included) no-op and
+  // km_batch_end restores the state after the last iteration that ran
+  {
+    const int rc = prep(c, c->C64_new);
+    if (rc != KM_OK) return rc;
+  }
+  std::swap(c->C64_cur, c->C64_new);
+  c->batch_n = slot + 1;
+  return KM_OK;
+}
+
+int km_batch_end(km_ctx* c, km_status* st, int64_t* counts, int32_t* n_ran) {
+  KM_REQUIRE(c && c->in_batch, KM_ERR_STATE, "km_batch_end: no open batch");
+  KM_REQUIRE(n_ran, KM_ERR_ARG, "km_batch_end: null n_ran");
+  KM_HIP(hipSetDevice(c->device));
+  const int m = c->batch_n;
+  if (m > 0) {
+    KM_HIP(hipMemcpyAsync(c->hist_host, c->hist, sizeof(km::DevStatus) * m, hipMemcpyDeviceToHost, c->stream));
+    KM_HIP(hipMemcpyAsync(c->hist_counts_host, c->hist_counts, sizeof(int64_t) * (size_t)c->g.k * m,
+                          hipMemcpyDeviceToHost, c->stream));
+  }
+  KM_HIP(hipMemsetAsync(c->gate, 0, sizeof(int), c->stream));  // later launches run again
+  KM_HIP(hipStreamSynchronize(c->stream));
+  c->in_batch = false;
+  c->batch_n = 0;
+  int ran = 0;
+  while (ran < m && c->hist_host[ran].ran) ++ran;
+  *n_ran = ran;
+  if (ran > 0) {
+    // the state after the last iteration that ran, before its commit (as
+    // after km_update): its old / new buffers, the new one's images prepared
+    c->C64_cur = c->slot_cur[ran - 1];
+    c->C64_new = c->slot_new[ran - 1];
+    // the iteration that raised the gate had its own prep gated too
+    c->prep_of = c->hist_host[ran - 1].stop ? nullptr : c->C64_new;
+  } else if (m > 0) {
+    c->C64_cur = c->slot_cur[0];
+    c->C64_new = c->slot_new[0];
+    c->prep_of = nullptr;
+  }
+  for (int i = 0; i < ran; ++i) {
+    const km::DevStatus& s = c->hist_host[i];
+    if (st) {
+      st[i].sse = s.sse;
+      st[i].max_shift = s.max_shift;
+      st[i].n_empty = s.n_empty;
+      st[i].nonfinite = s.nonfinite;
+      st[i].q_rerank = s.q_rerank;
+      st[i].q_full = s.q_full;
+      st[i].ran = s.ran;
+      st[i].stop_reason = s.stop;
+    }
+    if (counts) memcpy(counts + (size_t)i * c->g.k, c->hist_counts_host + (size_t)i * c->g.k, sizeof(int64_t) * c->g.k);
+  }
+  return KM_OK;
 }
 
 int km_replace_rows(km_ctx* c, const int32_t* ids, const double* rows, int32_t n) {

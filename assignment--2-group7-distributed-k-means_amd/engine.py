@@ -131,6 +131,22 @@ class HipEngine:
         self._c(self.lib.km_update(self.ctx, ctypes.byref(st), _ptr(counts, _PI64)), "km_update")
         return st, counts
 
+    # -- batches of iterations with one host sync (km_batch_*) -------------------
+    def batch_begin(self) -> None:
+        self._c(self.lib.km_batch_begin(self.ctx), "km_batch_begin")
+
+    def update_async(self, tol: float) -> None:
+        self._c(self.lib.km_update_async(self.ctx, float(tol)), "km_update_async")
+
+    def batch_end(self, m: int):
+        """Sync once; [(status, counts)] of the iterations of the batch that ran
+        (the rest were no-ops after the device stopped it)."""
+        st = (_lib.KmStatus * max(m, 1))()
+        counts = np.zeros((max(m, 1), self.k), dtype=np.int64)
+        n = ctypes.c_int32(0)
+        self._c(self.lib.km_batch_end(self.ctx, st, _ptr(counts, _PI64), ctypes.byref(n)), "km_batch_end")
+        return [(st[i], counts[i]) for i in range(n.value)]
+
     def replace_rows(self, ids, rows: np.ndarray) -> None:
         ids = np.ascontiguousarray(ids, dtype=np.int32)
         rows = np.ascontiguousarray(rows, dtype=np.float64).reshape(len(ids), self.d)

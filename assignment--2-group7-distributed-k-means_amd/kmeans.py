@@ -65,13 +65,74 @@ class LloydRunner:
             out[mine] = self.engine.gather_rows(gidx[mine] - lo)
         return self.comm.allreduce_np(out)
 
-    # -- one Lloyd iteration -----------------------------------------------------------
+    # -- Lloyd iterations ---------------------------------------------------------------
+    batch = 8  # iterations enqueued per host synchronisation (the device stops a batch early)
+
+    def run(self, model: "KMeans", log, max_iter: int, first: int = 0) -> bool:
+        """Iterations ``first .. max_iter-1`` of the loop of kmeans_spark.py:266-313,
+        in batches: per iteration assign + stats, the all-reduce and the update are
+        enqueued without host synchronisation; the device records each
+        iteration and stops the batch on convergence, empty clusters or
+        non-finite centroids.  The host then replays, from those records, the
+        per-iteration log lines and SSE history, and handles the last iteration
+        that ran exactly as ``iteration`` does.  Returns True on convergence."""
+        it = first
+        eng = self.engine
+        while it < max_iter:
+            m = min(self.batch, max_iter - it)
+            eng.batch_begin()
+            for _ in range(m):
+                eng.assign_stats()                             # L272 (+ L169-171 map side)
+                self.comm.allreduce_stats(eng)                 # L169-173 shuffle + collect
+                eng.update_async(model.tolerance)              # L176-188, device convergence test
+            recs = eng.batch_end(m)
+            for b, (st, counts) in enumerate(recs):
+                if b + 1 < len(recs):                          # ran through: committed on the device
+                    self._record(model, it, st, counts, st.max_shift, log)
+                elif self._after_update(model, it, st, counts, log):
+                    return True
+                it += 1
+        return False
+
     def iteration(self, model: "KMeans", iteration: int, log) -> bool:
-        """Returns True when converged (max_shift < tolerance)."""
-        eng, k = self.engine, self.k
+        """One Lloyd iteration with a host sync (kmeans_spark.py:266-318).
+        Returns True when converged (max_shift < tolerance)."""
+        eng = self.engine
         eng.assign_stats()                                     # L272 (+ L169-171 map side)
         self.comm.allreduce_stats(eng)                         # L169-173 shuffle + collect
         st, counts = eng.update()                              # L176-188 (+ SSE, shift)
+        return self._after_update(model, iteration, st, counts, log)
+
+    def _record(self, model, iteration, st, counts, max_shift, log) -> None:
+        """SSE history with its warning (L278-286), then the log line (L297-304)."""
+        self._sse(model, st, log)
+        self._log_line(model, iteration, st, counts, max_shift, log)
+
+    @staticmethod
+    def _sse(model, st, log) -> None:
+        if model.compute_sse:                                  # L278-286
+            sse = float(st.sse)
+            model.sse_history.append(sse)
+            if log and len(model.sse_history) > 1 and sse > model.sse_history[-2] + 1e-6:
+                log(f"  WARNING: SSE increased from {model.sse_history[-2]:.4f} to {sse:.4f}")
+
+    def _log_line(self, model, iteration, st, counts, max_shift, log) -> None:
+        if log:  # None when nothing is printed (not verbose, or not rank 0): skip the formatting
+            cluster_sizes = [int(c) for c in counts]           # L297
+            if model.compute_sse and model.sse_history:
+                log(f"Iteration {iteration + 1}: SSE = {model.sse_history[-1]:.4f}, "
+                    f"Max Shift = {max_shift:.6f}, Cluster Sizes = {cluster_sizes}")
+            else:
+                log(f"Iteration {iteration + 1}: Max Shift = {max_shift:.6f}, Cluster Sizes = {cluster_sizes}")
+        self.last = {"max_shift": max_shift, "sse": float(st.sse) if model.compute_sse else None,
+                     "counts": counts, "n_empty": int(st.n_empty), "q_rerank": int(st.q_rerank),
+                     "q_full": int(st.q_full)}
+
+    def _after_update(self, model, iteration, st, counts, log) -> bool:
+        """The rest of an iteration once the device update is done (state: new
+        centroids computed, not committed): empty repair, SSE, NaN check, log,
+        commit, convergence (kmeans_spark.py:191-313)."""
+        eng, k = self.engine, self.k
         max_shift = st.max_shift
         nonfinite = bool(st.nonfinite)
         if st.n_empty:                                         # L191
@@ -88,24 +149,11 @@ class LloydRunner:
                 shift = np.linalg.norm(reps[:len(ids)] - old[ids], axis=1)
                 max_shift = max(max_shift, float(np.max(shift)))
                 nonfinite = nonfinite or not np.all(np.isfinite(reps))
-        sse = None
-        if model.compute_sse:                                  # L278-286
-            sse = float(st.sse)
-            model.sse_history.append(sse)
-            if log and len(model.sse_history) > 1 and sse > model.sse_history[-2] + 1e-6:
-                log(f"  WARNING: SSE increased from {model.sse_history[-2]:.4f} to {sse:.4f}")
+        self._sse(model, st, log)                              # L278-286
         if nonfinite:                                          # L289-290
             raise ValueError(f"NaN or Inf detected in centroids at iteration {iteration + 1}")
-        if log:  # None when nothing is printed (not verbose, or not rank 0): skip the formatting
-            cluster_sizes = [int(c) for c in counts]           # L297
-            if model.compute_sse and model.sse_history:
-                log(f"Iteration {iteration + 1}: SSE = {model.sse_history[-1]:.4f}, "
-                    f"Max Shift = {max_shift:.6f}, Cluster Sizes = {cluster_sizes}")
-            else:
-                log(f"Iteration {iteration + 1}: Max Shift = {max_shift:.6f}, Cluster Sizes = {cluster_sizes}")
+        self._log_line(model, iteration, st, counts, max_shift, log)   # L293-304
         eng.commit()                                           # L307
-        self.last = {"max_shift": max_shift, "sse": sse, "counts": counts, "n_empty": int(st.n_empty),
-                     "q_rerank": int(st.q_rerank), "q_full": int(st.q_full)}
         if max_shift < model.tolerance:                        # L310-313
             if log:
                 log(f"Converged after {iteration + 1} iterations")
@@ -222,9 +270,7 @@ class KMeans:
         run.engine.set_centroids(np.asarray(self.centroids, dtype=np.float64))
         run.engine.set_sse(self.compute_sse)
         try:
-            for iteration in range(self.max_iter):             # L266
-                if run.iteration(self, iteration, say):
-                    break
+            run.run(self, say, self.max_iter)                  # L266-313
         finally:
             self.centroids = run.engine.get_centroids(0).astype(out_dtype, copy=False)
         return self

@@ -5,7 +5,9 @@
 
 A "step" is one Lloyd iteration of ``KMeans.fit`` (assign -> partial stats ->
 RCCL all-reduce -> update -> commit, kmeans_spark.py:266-318) over the
-workload's rows, which were generated in HBM before timing.  Default workload
+workload's rows, which were generated in HBM before timing; steps are
+enqueued in batches with one host synchronisation per batch, as ``fit`` runs
+them (``LloydRunner.run``).  Default workload
 = the metric's configuration, N=100M rows, d=64, k=256 (fits one MI355X: 25.6
 GB); the N rows are split over the ranks (strong scaling).  Rank 0 prints one
 JSON line with ``roofline`` (dominant kernel, HIP-event timed on its stream)
@@ -113,8 +115,10 @@ def main():
     log = None  # silent run: the loop skips formatting its log lines (kmeans.LloydRunner.iteration)
 
     import torch
-    for i in range(args.warmup):
-        run.iteration(km, i, log)
+    # iterations run in batches with one host sync each (LloydRunner.run: the
+    # device records every iteration and would stop a batch on convergence,
+    # empty clusters or NaN; tolerance 1e-300 never converges)
+    run.run(km, log, args.warmup)
     eng.sync()
     comm.barrier()
     torch.cuda.synchronize()
@@ -123,15 +127,13 @@ def main():
     # from two untimed steps after it
     eng.profile(True, phases=("assign", "stats"))
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        run.iteration(km, args.warmup + i, log)
+    run.run(km, log, args.warmup + args.steps, first=args.warmup)
     eng.sync()
     torch.cuda.synchronize()
     comm.barrier()
     t1 = time.perf_counter()
     eng.profile(True, phases=("resolve", "update", "prep"))
-    for i in range(2):
-        run.iteration(km, args.warmup + args.steps + i, log)
+    run.run(km, log, args.warmup + args.steps + 2, first=args.warmup + args.steps)
     eng.sync()
     eng.profile(False)
     dt = float(comm.allreduce_np(np.array([t1 - t0])).max()) if world == 1 else None

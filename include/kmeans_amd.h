@@ -51,7 +51,16 @@ typedef struct km_status {
   int32_t nonfinite; /* NaN/Inf in a new centroid (kmeans_spark.py:289)         */
   int32_t q_rerank;  /* points whose top-2 were re-ranked in float64             */
   int32_t q_full;    /* points that needed a full float64 scan                   */
+  int32_t ran;       /* 1: the iteration ran (0: a no-op of a stopped batch)     */
+  int32_t stop_reason; /* KM_STOP_* this iteration raised (batches), else 0     */
 } km_status;
+
+/* Why a batch stopped (km_status.stop_reason). */
+#define KM_STOP_CONVERGED 1 /* max_shift < tolerance (kmeans_spark.py:310)       */
+#define KM_STOP_EMPTY 2     /* empty clusters: host repair (kmeans_spark.py:191)  */
+#define KM_STOP_NONFINITE 3 /* NaN/Inf centroid (kmeans_spark.py:289)            */
+/* Iterations per batch (km_batch_begin .. km_batch_end). */
+#define KM_MAX_BATCH 32
 
 /* Static facts about a context (for logging / benchmarks). */
 typedef struct km_info {
@@ -127,6 +136,20 @@ int km_bind_stats_buffer(km_ctx* ctx, void* dev_ptr);
  * Returns KM_EMPTY when clusters are empty (their new centroid is the old
  * one until km_replace_rows). */
 int km_update(km_ctx* ctx, km_status* st, int64_t* counts);
+/* Batches of Lloyd iterations without host synchronisation (replaces the
+ * per-iteration driver round trip of kmeans_spark.py:266-313).  Between
+ * km_batch_begin and km_batch_end the caller enqueues up to KM_MAX_BATCH
+ * iterations, each km_assign_stats [+ its all-reduce of the stats buffer] +
+ * km_update_async(tol); km_update_async also commits speculatively.  The
+ * device records every iteration (status, counts) and, on convergence
+ * (max_shift < tol), empty clusters or non-finite centroids, raises a gate
+ * that turns the rest of the batch into no-ops.  km_batch_end synchronises
+ * once, returns the records of the iterations that ran (*n_ran of them:
+ * st[i], counts[i*k .. i*k+k)) and leaves the context as km_update would
+ * after the last of them: km_replace_rows / km_commit apply to it. */
+int km_batch_begin(km_ctx* ctx);
+int km_update_async(km_ctx* ctx, double tol);
+int km_batch_end(km_ctx* ctx, km_status* st, int64_t* counts, int32_t* n_ran);
 /* Empty-cluster repair (kmeans_spark.py:196-204): overwrite new centroids
  * of the given clusters with the given rows (float64 [n][d]). */
 int km_replace_rows(km_ctx* ctx, const int32_t* cluster_ids, const double* rows, int32_t n);

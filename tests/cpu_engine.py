@@ -46,7 +46,28 @@ class OracleEngine:
     def get_centroids(self, which=0):
         return (self.new if which else self.cur).copy()
 
+    # batches (mirror of km_batch_begin / km_update_async / km_batch_end) --------------
+    def batch_begin(self):
+        self._batching, self._stopped, self._slots = True, False, []
+
+    def update_async(self, tol):
+        if self._stopped:
+            return
+        st, counts = self.update()
+        stop = 3 if st.nonfinite else (2 if st.n_empty else (1 if st.max_shift < tol else 0))
+        self._slots.append((self.cur.copy(), self.new.copy(), st, counts))
+        self._stopped = bool(stop)
+        self.cur = self.new.copy()                      # speculative commit
+
+    def batch_end(self, m):
+        if self._slots:                                 # state after the last iteration that ran
+            self.cur, self.new = self._slots[-1][0].copy(), self._slots[-1][1].copy()
+        self._batching = self._stopped = False
+        return [(st, counts) for _, _, st, counts in self._slots]
+
     def assign_stats(self):
+        if getattr(self, "_stopped", False):            # a stopped batch: no-op
+            return
         import torch
         S = np.zeros(self.k * (self.d + 1) + 1)
         T = S[:-1].reshape(self.k, self.d + 1)
