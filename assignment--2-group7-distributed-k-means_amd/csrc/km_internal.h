@@ -54,6 +54,9 @@ hipError_t launch_prep_centroids(const double* C64, const Geometry& g, float* C3
                                  float* cabs, double* C64T, double* C64P, const int* gate, hipStream_t s);
 // fp16 hi/lo split of -2*c*s and ||c||^2 s^2 for the MFMA screen (s from the
 // data and centroid abs maxima)
+// the small path's images only (fp32 copy + max norm), one launch
+hipError_t launch_prep_small(const double* C64, const Geometry& g, float* C32, float* cmax, const int* gate,
+                             hipStream_t s);
 hipError_t launch_prep_split(const float* C32, const Geometry& g, const float* cn2, const float* xabs,
                              const float* cabs, _Float16* Chi, _Float16* Clo, float* cn2s, const int* gate, hipStream_t s);
 hipError_t launch_absmax(const float* X, int64_t nfloats, float* out, hipStream_t s);

@@ -121,6 +121,40 @@ __global__ __launch_bounds__(64) void k_prep_centroids(const double* __restrict_
   }
 }
 
+// Small path (k <= 32, dp <= 64): its only centroid images -- the fp32 copy
+// [kp][dp] and max ||c|| -- in one workgroup (the MFMA path's prep is four
+// launches: maxima, copies + norms, fp16 split, bound constants)
+__global__ __launch_bounds__(256) void k_prep_small(const double* __restrict__ C64, int k, int d, int dp, int kp,
+                                                    float* __restrict__ C32, float* __restrict__ cmax,
+                                                    const int* __restrict__ gate) {
+  if (*gate) return;
+  __shared__ unsigned int red[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned int mx = 0u;  // max of non-negative floats (or NaN) as bits, like the atomicMax of k_prep_centroids
+  for (int j = wave; j < kp; j += 4) {
+    double nn = 0.0;
+    for (int f = lane; f < dp; f += 64) {
+      const double c = (j < k && f < d) ? C64[(size_t)j * d + f] : 0.0;
+      nn = fma(c, c, nn);
+      C32[(size_t)j * dp + f] = (float)c;
+    }
+    nn = wave_sum(nn);
+    if (lane == 0 && j < k) {
+      const float cn = sqrtf((float)nn) * 1.0001f + 1e-30f;
+      mx = max(mx, __float_as_uint(cn));
+    }
+  }
+  if (lane == 0) red[wave] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) *cmax = __uint_as_float(max(max(red[0], red[1]), max(red[2], red[3])));
+}
+
+hipError_t launch_prep_small(const double* C64, const Geometry& g, float* C32, float* cmax, const int* gate,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(k_prep_small, dim3(1), dim3(256), 0, s, C64, g.k, g.d, g.dp, g.kp, C32, cmax, gate);
+  return hipGetLastError();
+}
+
 __global__ void k_zero_maxima(float* __restrict__ cmax, float* __restrict__ cabs, const int* __restrict__ gate) {
   if (*gate) return;
   if (threadIdx.x == 0) {
@@ -2385,9 +2419,104 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ wor
   }
 }
 
+// k_update + k_finalize in one workgroup for small k (c1 / c2 shapes, where
+// the two launches are mostly launch gaps): same arithmetic and
+// reduction order per cluster (lanes over features, wave sums), then the
+// status record and the batch gate as k_finalize.
+__global__ __launch_bounds__(1024) void k_update_one(const double* __restrict__ stats, const double* __restrict__ old,
+                                                     int k, int d, double* __restrict__ out,
+                                                     int64_t* __restrict__ counts, const double* __restrict__ sse,
+                                                     const uint32_t* __restrict__ qcount, uint32_t nq,
+                                                     DevStatus* __restrict__ st, int* __restrict__ gate,
+                                                     double stop_tol) {
+  if (*gate) {
+    if (threadIdx.x == 0) {
+      st->ran = 0;
+      st->stop = 0;
+    }
+    return;
+  }
+  __shared__ double s_max[16];
+  __shared__ int s_emp[16], s_nf[16], s_q[16], s_qf[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int d1 = d + 1;
+  double mx = 0.0;
+  int emp = 0, nf = 0, qa = 0, qb = 0;
+  for (int j = wave; j < k; j += nw) {
+    const double cnt = stats[(size_t)j * d1 + d];
+    double sh = 0.0, nfl = 0.0;
+    for (int f = lane; f < d; f += 64) {
+      const double S = stats[(size_t)j * d1 + f];
+      const double o = old[(size_t)j * d + f];
+      const double nv = (cnt > 0.0) ? S / cnt : o;
+      out[(size_t)j * d + f] = nv;
+      const double df = nv - o;
+      sh = fma(df, df, sh);
+      if (!isfinite(nv)) nfl = 1.0;
+    }
+    sh = wave_sum(sh);
+    nfl = wave_sum(nfl);
+    if (lane == 0) {
+      counts[j] = (int64_t)cnt;
+      mx = fmax(mx, sh);
+      nf |= (nfl != 0.0);
+      emp += (cnt == 0.0);
+    }
+  }
+  for (uint32_t w = threadIdx.x; w < nq; w += blockDim.x) {
+    qa += (int)qcount[2 * w];
+    qb += (int)qcount[2 * w + 1];
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    qa += __shfl_xor(qa, o);
+    qb += __shfl_xor(qb, o);
+  }
+  if (lane == 0) {
+    s_max[wave] = mx;
+    s_emp[wave] = emp;
+    s_nf[wave] = nf;
+    s_q[wave] = qa;
+    s_qf[wave] = qb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < nw; ++w) {
+      mx = fmax(mx, s_max[w]);
+      emp += s_emp[w];
+      nf |= s_nf[w];
+      qa += s_q[w];
+      qb += s_qf[w];
+    }
+    const double ms = sqrt(mx);
+    st->max_shift = ms;
+    st->sse = *sse;
+    st->n_empty = emp;
+    st->nonfinite = nf;
+    st->q_full = qb;
+    st->q_rerank = qa;
+    st->ran = 1;
+    int stop = 0;
+    if (stop_tol >= 0.0) {
+      if (nf)
+        stop = KM_STOP_NONFINITE;
+      else if (emp)
+        stop = KM_STOP_EMPTY;
+      else if (ms < stop_tol)
+        stop = KM_STOP_CONVERGED;
+    }
+    st->stop = stop;
+    if (stop) *gate = stop;
+  }
+}
+
 hipError_t launch_update(const double* stats, const double* C64_old, const Geometry& g, double* C64_new,
                          double* work, int64_t* counts, const uint32_t* qcount, uint32_t nq, DevStatus* status,
                          int* gate, double stop_tol, hipStream_t s) {
+  if (g.k <= 64 && (size_t)g.k * g.d <= 16384) {  // at most 4 clusters per wave (c3: 2 launches, 11 vs 37 us)
+    hipLaunchKernelGGL(k_update_one, dim3(1), dim3(1024), 0, s, stats, C64_old, g.k, g.d, C64_new, counts,
+                       stats + (size_t)g.k * (g.d + 1), qcount, nq, status, gate, stop_tol);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_update, dim3(g.k), dim3(64), 0, s, stats, C64_old, g.k, g.d, C64_new, work, counts, gate);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

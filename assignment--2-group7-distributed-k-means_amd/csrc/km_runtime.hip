@@ -221,6 +221,10 @@ void free_data(km_ctx* c) {
 int prep(km_ctx* c, const double* src) {
   ProfScope ps(c, KM_K_PREP);
   c->prep_of = src;
+  if (c->path == 1) {
+    KM_HIP(km::launch_prep_small(src, c->g, c->C32, c->cmax, c->gate, c->stream));
+    return KM_OK;
+  }
   KM_HIP(km::launch_prep_centroids(src, c->g, c->C32, c->cn2, c->cmax, c->cabs, c->C64T, c->C64P, c->gate,
                                    c->stream));
   KM_HIP(km::launch_prep_split(c->C32, c->g, c->cn2, c->xabs, c->cabs, c->Chi, c->Clo, c->cn2s, c->gate, c->stream));

@@ -24,7 +24,7 @@ from typing import List, Optional
 
 import numpy as np
 
-from . import sampling
+from . import _lib, sampling
 from .comm import Communicator
 from .dataset import DeviceBlobs, LocalRDD, Placement, place
 from .engine import make_engine
@@ -66,7 +66,7 @@ class LloydRunner:
         return self.comm.allreduce_np(out)
 
     # -- Lloyd iterations ---------------------------------------------------------------
-    batch = 8  # iterations enqueued per host synchronisation (the device stops a batch early)
+    batch = 4  # first batch size; doubles (to KM_MAX_BATCH) while batches run through
 
     def run(self, model: "KMeans", log, max_iter: int, first: int = 0) -> bool:
         """Iterations ``first .. max_iter-1`` of the loop of kmeans_spark.py:266-313,
@@ -78,14 +78,18 @@ class LloydRunner:
         that ran exactly as ``iteration`` does.  Returns True on convergence."""
         it = first
         eng = self.engine
+        size = self.batch
         while it < max_iter:
-            m = min(self.batch, max_iter - it)
+            m = min(size, max_iter - it)
             eng.batch_begin()
             for _ in range(m):
                 eng.assign_stats()                             # L272 (+ L169-171 map side)
                 self.comm.allreduce_stats(eng)                 # L169-173 shuffle + collect
                 eng.update_async(model.tolerance)              # L176-188, device convergence test
             recs = eng.batch_end(m)
+            # a batch that ran through doubles the next one (fewer host round
+            # trips on long runs); a stopped one (convergence, empties) resets it
+            size = min(2 * size, _lib.KM_MAX_BATCH) if len(recs) == m and not recs[-1][0].stop_reason else self.batch
             for b, (st, counts) in enumerate(recs):
                 if b + 1 < len(recs):                          # ran through: committed on the device
                     self._record(model, it, st, counts, st.max_shift, log)

@@ -55,6 +55,7 @@ class OracleEngine:
             return
         st, counts = self.update()
         stop = 3 if st.nonfinite else (2 if st.n_empty else (1 if st.max_shift < tol else 0))
+        st.stop_reason = stop
         self._slots.append((self.cur.copy(), self.new.copy(), st, counts))
         self._stopped = bool(stop)
         self.cur = self.new.copy()                      # speculative commit
@@ -93,7 +94,8 @@ class OracleEngine:
         self.new = new
         shift = np.sqrt(((new - old) ** 2).sum(axis=1))
         st = _Status(sse=float(flat[-1]), max_shift=float(shift.max()), n_empty=int((cnt == 0).sum()),
-                     nonfinite=int(not np.all(np.isfinite(new))), q_rerank=0, q_full=0)
+                     nonfinite=int(not np.all(np.isfinite(new))), q_rerank=0, q_full=0, ran=1,
+                     stop_reason=0)
         return st, cnt.astype(np.int64)
 
     def replace_rows(self, ids, rows):
