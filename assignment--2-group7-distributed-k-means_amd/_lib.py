@@ -33,7 +33,8 @@ KM_MAX_BATCH = 32
 class KmStatus(ctypes.Structure):
     _fields_ = [("sse", ctypes.c_double), ("max_shift", ctypes.c_double), ("n_empty", ctypes.c_int32),
                 ("nonfinite", ctypes.c_int32), ("q_rerank", ctypes.c_int32), ("q_full", ctypes.c_int32),
-                ("ran", ctypes.c_int32), ("stop_reason", ctypes.c_int32)]
+                ("ran", ctypes.c_int32), ("stop_reason", ctypes.c_int32), ("repaired", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 class KmInfo(ctypes.Structure):
@@ -72,7 +73,8 @@ SIGNATURES = {
     "km_bind_stats_buffer": [_P, _P],
     "km_update": [_P, ctypes.POINTER(KmStatus), _PI64],
     "km_batch_begin": [_P],
-    "km_update_async": [_P, _D],
+    "km_update_async": [_P, _D, _I64],
+    "km_set_layout": [_P, _PI64, _I32, _I64, _I32],
     "km_batch_end": [_P, ctypes.POINTER(KmStatus), _PI64, _PI32],
     "km_replace_rows": [_P, _PI32, _PD, _I32],
     "km_commit": [_P],

@@ -29,8 +29,11 @@ struct DevStatus {
   int32_t q_full;      // screened points that needed the full exact scan
   int32_t ran;         // 0: the iteration was a no-op of a stopped batch
   int32_t stop;        // KM_STOP_* raised by this iteration (batches)
+  int32_t repaired;    // empty clusters were replaced on the device (max_shift includes them)
+  int32_t pad;
 };
-static_assert(sizeof(DevStatus) == 40, "layout of km_status");
+static_assert(sizeof(DevStatus) == 48, "layout of km_status");
+
 
 // Per-wave segments of the ambiguous-point queue written by k_assign_mfma:
 // wave w owns entries [w*seg, w*seg + qcount[2w]); qcount[2w+1] = full scans.
@@ -116,12 +119,21 @@ hipError_t launch_sse(const float* X, const Geometry& g, const int32_t* labels, 
 // stats = [k][d+1] sums and counts, then the SSE slot stats[k (d+1)]
 // gate: the batch's stop flag (kernels of later iterations no-op once it is
 // set); stop_tol >= 0 lets k_finalize raise it (KM_STOP_*), < 0 never
+// dev_repair: empty clusters are repaired on the device (launch_repair), so
+// they neither raise the gate nor allow a convergence stop here
 hipError_t launch_update(const double* stats, const double* C64_old, const Geometry& g, double* C64_new,
                          double* work, int64_t* counts, const uint32_t* qcount, uint32_t nq, DevStatus* status,
-                         int* gate, double stop_tol, hipStream_t s);
+                         int* gate, double stop_tol, int dev_repair, hipStream_t s);
 hipError_t launch_sum_x(const float* X, const Geometry& g, double* out, hipStream_t s);
 hipError_t launch_gather_rows(const float* X, const Geometry& g, const int64_t* idx, int32_t n, double* out,
                               hipStream_t s);
+// on-device empty-cluster repair after the update of one iteration: the
+// Bernoulli passes, then one workgroup for the rest (km_sample.hip); no-ops
+// unless the update left empty clusters and the gate is down
+hipError_t launch_repair(int* gate, const int64_t* counts, const Geometry& g, int64_t total, double neg_log_delta,
+                         uint64_t seed, int32_t* empty, int32_t* pcounts, int64_t* picks, int64_t* samples, int cp,
+                         const int64_t* sizes, const int64_t* bases, int nparts, const float* X, int64_t row0,
+                         const double* C_old, double* C_new, DevStatus* st, double tol, hipStream_t s);
 // takeSample's Bernoulli pass, one wave per partition (km_sample.hip)
 hipError_t launch_bernoulli(const uint64_t* seeds, const int64_t* sizes, const int64_t* bases, int nparts,
                             double fraction, int64_t* out, int cp, int32_t* counts, hipStream_t s);

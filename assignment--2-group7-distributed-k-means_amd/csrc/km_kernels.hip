@@ -2359,7 +2359,7 @@ __global__ __launch_bounds__(64) void k_update(const double* __restrict__ stats,
 __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ work, const int64_t* __restrict__ counts,
                                                   int k, const double* __restrict__ sse,
                                                   const uint32_t* __restrict__ qcount, uint32_t nq,
-                                                  DevStatus* __restrict__ st, int* __restrict__ gate, double stop_tol) {
+                                                  DevStatus* __restrict__ st, int* __restrict__ gate, double stop_tol, int dev_repair) {
   if (*gate) {
     if (threadIdx.x == 0) {
       st->ran = 0;
@@ -2410,10 +2410,11 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ wor
       if (s_nf[0])
         stop = KM_STOP_NONFINITE;
       else if (s_emp[0])
-        stop = KM_STOP_EMPTY;
+        stop = dev_repair ? 0 : KM_STOP_EMPTY;  // repaired next, which then decides
       else if (ms < stop_tol)
         stop = KM_STOP_CONVERGED;
     }
+    st->repaired = 0;
     st->stop = stop;
     if (stop) *gate = stop;
   }
@@ -2428,7 +2429,7 @@ __global__ __launch_bounds__(1024) void k_update_one(const double* __restrict__ 
                                                      int64_t* __restrict__ counts, const double* __restrict__ sse,
                                                      const uint32_t* __restrict__ qcount, uint32_t nq,
                                                      DevStatus* __restrict__ st, int* __restrict__ gate,
-                                                     double stop_tol) {
+                                                     double stop_tol, int dev_repair) {
   if (*gate) {
     if (threadIdx.x == 0) {
       st->ran = 0;
@@ -2500,10 +2501,11 @@ __global__ __launch_bounds__(1024) void k_update_one(const double* __restrict__ 
       if (nf)
         stop = KM_STOP_NONFINITE;
       else if (emp)
-        stop = KM_STOP_EMPTY;
+        stop = dev_repair ? 0 : KM_STOP_EMPTY;  // repaired next, which then decides
       else if (ms < stop_tol)
         stop = KM_STOP_CONVERGED;
     }
+    st->repaired = 0;
     st->stop = stop;
     if (stop) *gate = stop;
   }
@@ -2511,17 +2513,17 @@ __global__ __launch_bounds__(1024) void k_update_one(const double* __restrict__ 
 
 hipError_t launch_update(const double* stats, const double* C64_old, const Geometry& g, double* C64_new,
                          double* work, int64_t* counts, const uint32_t* qcount, uint32_t nq, DevStatus* status,
-                         int* gate, double stop_tol, hipStream_t s) {
+                         int* gate, double stop_tol, int dev_repair, hipStream_t s) {
   if (g.k <= 64 && (size_t)g.k * g.d <= 16384) {  // at most 4 clusters per wave (c3: 2 launches, 11 vs 37 us)
     hipLaunchKernelGGL(k_update_one, dim3(1), dim3(1024), 0, s, stats, C64_old, g.k, g.d, C64_new, counts,
-                       stats + (size_t)g.k * (g.d + 1), qcount, nq, status, gate, stop_tol);
+                       stats + (size_t)g.k * (g.d + 1), qcount, nq, status, gate, stop_tol, dev_repair);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_update, dim3(g.k), dim3(64), 0, s, stats, C64_old, g.k, g.d, C64_new, work, counts, gate);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, work, counts, g.k, stats + (size_t)g.k * (g.d + 1),
-                     qcount, nq, status, gate, stop_tol);
+                     qcount, nq, status, gate, stop_tol, dev_repair);
   return hipGetLastError();
 }
 

@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <string>
 #include <utility>
 #include <vector>
@@ -122,6 +123,18 @@ struct km_ctx {
   int batch_n = 0;
   double* slot_cur[KM_MAX_BATCH] = {};
   double* slot_new[KM_MAX_BATCH] = {};
+  // on-device empty-cluster repair (km_set_layout): the dataset's takeSample
+  // partition layout and the repair's work buffers
+  bool rep_enabled = false;
+  int rep_nparts = 0;
+  int64_t rep_total = 0, rep_row0 = 0, rep_maxpart = 0;
+  int64_t* rep_sizes = nullptr;   // device [nparts]
+  int64_t* rep_bases = nullptr;   // device [nparts]
+  int rep_cp = 0, rep_k = 0;      // pick slots per partition, k they were sized for
+  int32_t* rep_empty = nullptr;   // [k]
+  int32_t* rep_pcounts = nullptr; // [nparts]
+  int64_t* rep_picks = nullptr;   // [nparts][cp]
+  int64_t* rep_samples = nullptr; // [nparts * cp]
   // staging
   float* pinned = nullptr;
   size_t pinned_floats = 0;
@@ -243,6 +256,42 @@ int ensure_scratch(km_ctx* c, int64_t rows) {
 }
 
 int prep(km_ctx* c) { return prep(c, c->C64_cur); }
+
+void free_repair(km_ctx* c) {
+  dfree(c->rep_empty);
+  dfree(c->rep_pcounts);
+  dfree(c->rep_picks);
+  dfree(c->rep_samples);
+  c->rep_cp = 0;
+  c->rep_k = 0;
+}
+
+// takeSample's fraction for num rows of total (sampling.py _fraction)
+double sample_fraction(int64_t num, int64_t total) {
+  const double fraction = (double)num / (double)total;
+  const double gamma = -std::log(0.00005) / (double)total;
+  return std::min(1.0, fraction + gamma + std::sqrt(gamma * gamma + 2.0 * gamma * fraction));
+}
+
+// repair buffers sized for the largest repair (all k clusters empty): per
+// partition 4x the expected picks + 64 slots (more -> the host repairs)
+int ensure_repair(km_ctx* c) {
+  if (c->rep_k == c->g.k && c->rep_pcounts) return KM_OK;
+  free_repair(c);
+  const double f = sample_fraction(std::min<int64_t>(c->g.k, std::max<int64_t>(c->rep_total - 1, 1)),
+                                   std::max<int64_t>(c->rep_total, 1));
+  const double cpd = 4.0 * f * (double)c->rep_maxpart + 64.0;
+  KM_REQUIRE(cpd < (double)(1 << 26), KM_ERR_ARG, "km_update_async: repair buffers too large");
+  c->rep_cp = (int)cpd;
+  const size_t slots = (size_t)c->rep_cp * c->rep_nparts;
+  KM_HIP(hipMalloc(&c->rep_empty, sizeof(int32_t) * c->g.k));
+  KM_HIP(hipMalloc(&c->rep_pcounts, sizeof(int32_t) * c->rep_nparts));
+  KM_HIP(hipMemsetAsync(c->rep_pcounts, 0, sizeof(int32_t) * c->rep_nparts, c->stream));
+  KM_HIP(hipMalloc(&c->rep_picks, sizeof(int64_t) * slots));
+  KM_HIP(hipMalloc(&c->rep_samples, sizeof(int64_t) * slots));
+  c->rep_k = c->g.k;
+  return KM_OK;
+}
 
 int run_assign(km_ctx* c, bool with_stats) {
   const km::Geometry& g = c->g;
@@ -372,6 +421,9 @@ int km_destroy(km_ctx* c) {
     }
   for (auto e : c->pool) (void)hipEventDestroy(e);
   dfree(c->gate);
+  free_repair(c);
+  dfree(c->rep_sizes);
+  dfree(c->rep_bases);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return KM_OK;
@@ -586,7 +638,7 @@ int km_update(km_ctx* c, km_status* st, int64_t* counts) {
   {
     ProfScope ps(c, KM_K_UPDATE);
     KM_HIP(km::launch_update(c->stats, c->C64_cur, c->g, c->C64_new, c->work, c->counts_dev, c->qcount,
-                             c->ql.nwaves, c->status_dev, c->gate, -1.0, c->stream));
+                             c->ql.nwaves, c->status_dev, c->gate, -1.0, 0, c->stream));
   }
   KM_HIP(hipMemcpyAsync(c->status_host, c->status_dev, sizeof(km::DevStatus), hipMemcpyDeviceToHost, c->stream));
   KM_HIP(hipMemcpyAsync(c->counts_host, c->counts_dev, sizeof(int64_t) * c->g.k, hipMemcpyDeviceToHost, c->stream));
@@ -607,9 +659,43 @@ int km_update(km_ctx* c, km_status* st, int64_t* counts) {
     st->q_full = s.q_full;
     st->ran = s.ran;
     st->stop_reason = s.stop;
+    st->repaired = 0;
   }
   if (counts) memcpy(counts, c->counts_host, sizeof(int64_t) * c->g.k);
   return s.n_empty > 0 ? KM_EMPTY : KM_OK;
+}
+
+int km_set_layout(km_ctx* c, const int64_t* sizes, int32_t nparts, int64_t row0, int32_t device_repair) {
+  KM_REQUIRE(c && c->loaded, KM_ERR_STATE, "km_set_layout: load data first");
+  KM_REQUIRE(nparts >= 0 && (nparts == 0 || sizes), KM_ERR_ARG, "km_set_layout: bad partitions");
+  KM_HIP(hipSetDevice(c->device));
+  KM_HIP(hipStreamSynchronize(c->stream));
+  free_repair(c);
+  dfree(c->rep_sizes);
+  dfree(c->rep_bases);
+  c->rep_enabled = false;
+  c->rep_nparts = nparts;
+  c->rep_total = 0;
+  c->rep_maxpart = 0;
+  c->rep_row0 = row0;
+  std::vector<int64_t> bases(nparts);
+  for (int i = 0; i < nparts; ++i) {
+    KM_REQUIRE(sizes[i] >= 0, KM_ERR_ARG, "km_set_layout: negative partition size");
+    bases[i] = c->rep_total;
+    c->rep_total += sizes[i];
+    c->rep_maxpart = std::max(c->rep_maxpart, sizes[i]);
+  }
+  if (device_repair) {
+    // every replacement row must be resident here (one rank holding all rows)
+    KM_REQUIRE(row0 == 0 && c->rep_total == c->g.n && nparts > 0, KM_ERR_ARG,
+               "km_set_layout: device repair needs every row of the dataset on this context");
+    KM_HIP(hipMalloc(&c->rep_sizes, sizeof(int64_t) * nparts));
+    KM_HIP(hipMalloc(&c->rep_bases, sizeof(int64_t) * nparts));
+    KM_HIP(hipMemcpy(c->rep_sizes, sizes, sizeof(int64_t) * nparts, hipMemcpyHostToDevice));
+    KM_HIP(hipMemcpy(c->rep_bases, bases.data(), sizeof(int64_t) * nparts, hipMemcpyHostToDevice));
+    c->rep_enabled = true;
+  }
+  return KM_OK;
 }
 
 int km_batch_begin(km_ctx* c) {
@@ -622,7 +708,7 @@ int km_batch_begin(km_ctx* c) {
   return KM_OK;
 }
 
-int km_update_async(km_ctx* c, double tol) {
+int km_update_async(km_ctx* c, double tol, int64_t empty_seed) {
   KM_REQUIRE(c && c->have_c && c->in_batch, KM_ERR_STATE, "km_update_async: call km_batch_begin first");
   KM_REQUIRE(c->batch_n < KM_MAX_BATCH, KM_ERR_ARG, "km_update_async: more than KM_MAX_BATCH iterations in a batch");
   KM_REQUIRE(tol >= 0.0, KM_ERR_ARG, "km_update_async: tolerance must be >= 0");
@@ -632,7 +718,16 @@ int km_update_async(km_ctx* c, double tol) {
     ProfScope ps(c, KM_K_UPDATE);
     KM_HIP(km::launch_update(c->stats, c->C64_cur, c->g, c->C64_new, c->work,
                              c->hist_counts + (size_t)slot * c->g.k, c->qcount, c->ql.nwaves, c->hist + slot,
-                             c->gate, tol, c->stream));
+                             c->gate, tol, c->rep_enabled ? 1 : 0, c->stream));
+  }
+  if (c->rep_enabled) {
+    KM_REQUIRE(empty_seed >= 0, KM_ERR_ARG, "km_update_async: negative empty-cluster seed");
+    const int rc = ensure_repair(c);
+    if (rc != KM_OK) return rc;
+    KM_HIP(km::launch_repair(c->gate, c->hist_counts + (size_t)slot * c->g.k, c->g, c->rep_total,
+                             -std::log(0.00005), (uint64_t)empty_seed, c->rep_empty, c->rep_pcounts, c->rep_picks,
+                             c->rep_samples, c->rep_cp, c->rep_sizes, c->rep_bases, c->rep_nparts, c->X,
+                             c->rep_row0, c->C64_cur, c->C64_new, c->hist + slot, tol, c->stream));
   }
   c->slot_cur[slot] = c->C64_cur;
   c->slot_new[slot] = c->C64_new;
@@ -688,6 +783,7 @@ int km_batch_end(km_ctx* c, km_status* st, int64_t* counts, int32_t* n_ran) {
       st[i].q_full = s.q_full;
       st[i].ran = s.ran;
       st[i].stop_reason = s.stop;
+      st[i].repaired = s.repaired;
     }
     if (counts) memcpy(counts + (size_t)i * c->g.k, c->hist_counts_host + (size_t)i * c->g.k, sizeof(int64_t) * c->g.k);
   }

@@ -135,8 +135,15 @@ class HipEngine:
     def batch_begin(self) -> None:
         self._c(self.lib.km_batch_begin(self.ctx), "km_batch_begin")
 
-    def update_async(self, tol: float) -> None:
-        self._c(self.lib.km_update_async(self.ctx, float(tol)), "km_update_async")
+    def update_async(self, tol: float, empty_seed: int = 0) -> None:
+        self._c(self.lib.km_update_async(self.ctx, float(tol), int(empty_seed)), "km_update_async")
+
+    def set_layout(self, sizes, row0: int, device_repair: bool) -> None:
+        """The dataset's takeSample partition layout; device_repair moves the
+        empty-cluster repair onto the GPU (one rank holding every row)."""
+        sizes = np.ascontiguousarray(sizes, dtype=np.int64)
+        self._c(self.lib.km_set_layout(self.ctx, _ptr(sizes, _PI64), len(sizes), int(row0), 1 if device_repair else 0),
+                "km_set_layout")
 
     def batch_end(self, m: int):
         """Sync once; [(status, counts)] of the iterations of the batch that ran

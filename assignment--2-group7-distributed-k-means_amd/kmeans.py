@@ -40,6 +40,7 @@ class LloydRunner:
         self.comm = comm
         self.k = k
         self.last = None
+        self.device_repairs = 0  # iterations whose empty clusters the device replaced
         # takeSample's Bernoulli pass on the GPU when the engine has one
         self.sampler = getattr(engine, "bernoulli", None)
 
@@ -51,6 +52,11 @@ class LloydRunner:
             self.engine.load_blobs(pl.n_local, b.d, pl.row0, b.n_centers, b.box, b.std, b.seed)
         else:
             self.engine.load_host(pl.local_rows)
+        # one rank holding every row: empty clusters are repaired on the device
+        # (takeSample policy, kmeans_spark.py:191-204) without stopping a batch
+        self.device_repair = self.comm.world == 1 and hasattr(self.engine, "set_layout")
+        if self.device_repair:
+            self.engine.set_layout(pl.global_sizes, 0, True)
 
     def rows(self, gidx: List[int]) -> np.ndarray:
         """Rows by global index (what ``rdd.takeSample`` returns, L72/L196)."""
@@ -85,7 +91,8 @@ class LloydRunner:
             for _ in range(m):
                 eng.assign_stats()                             # L272 (+ L169-171 map side)
                 self.comm.allreduce_stats(eng)                 # L169-173 shuffle + collect
-                eng.update_async(model.tolerance)              # L176-188, device convergence test
+                # L176-206 (+ the repair's seed int(time.time()), L196), device convergence test
+                eng.update_async(model.tolerance, model._empty_seed())
             recs = eng.batch_end(m)
             # a batch that ran through doubles the next one (fewer host round
             # trips on long runs); a stopped one (convergence, empties) resets it
@@ -108,7 +115,13 @@ class LloydRunner:
         return self._after_update(model, iteration, st, counts, log)
 
     def _record(self, model, iteration, st, counts, max_shift, log) -> None:
-        """SSE history with its warning (L278-286), then the log line (L297-304)."""
+        """An iteration that ran through on the device: the empty-cluster
+        warning if the device repaired some (L192), SSE history with its
+        warning (L278-286), then the log line (L297-304)."""
+        if st.n_empty:
+            self.device_repairs += 1
+            if log:
+                log(f"  WARNING: {int(st.n_empty)} empty cluster(s) detected. Reinitializing...")
         self._sse(model, st, log)
         self._log_line(model, iteration, st, counts, max_shift, log)
 
@@ -139,7 +152,11 @@ class LloydRunner:
         eng, k = self.engine, self.k
         max_shift = st.max_shift
         nonfinite = bool(st.nonfinite)
-        if st.n_empty:                                         # L191
+        if st.n_empty and getattr(st, "repaired", 0):          # L191-204 done on the device
+            self.device_repairs += 1
+            if log:
+                log(f"  WARNING: {int(st.n_empty)} empty cluster(s) detected. Reinitializing...")
+        elif st.n_empty:                                       # L191
             empty = [j for j in range(k) if counts[j] == 0]
             if log:
                 log(f"  WARNING: {len(empty)} empty cluster(s) detected. Reinitializing...")

@@ -53,6 +53,9 @@ typedef struct km_status {
   int32_t q_full;    /* points that needed a full float64 scan                   */
   int32_t ran;       /* 1: the iteration ran (0: a no-op of a stopped batch)     */
   int32_t stop_reason; /* KM_STOP_* this iteration raised (batches), else 0     */
+  int32_t repaired;  /* its empty clusters were replaced on the device
+                        (max_shift includes them, kmeans_spark.py:191-204)      */
+  int32_t reserved;
 } km_status;
 
 /* Why a batch stopped (km_status.stop_reason). */
@@ -136,11 +139,24 @@ int km_bind_stats_buffer(km_ctx* ctx, void* dev_ptr);
  * Returns KM_EMPTY when clusters are empty (their new centroid is the old
  * one until km_replace_rows). */
 int km_update(km_ctx* ctx, km_status* st, int64_t* counts);
+/* The dataset's partition layout for rdd.takeSample (sizes[nparts] in row
+ * order; this context's rows start at global row row0).  device_repair = 1
+ * (one context holding every row) moves the empty-cluster repair of
+ * kmeans_spark.py:191-204 onto the device inside batches: after an update
+ * with empty clusters, takeSample(False, n_empty, empty_seed) runs there
+ * (PySpark's fraction, per-partition Bernoulli passes with CPython's MT19937,
+ * retry, shuffle), its rows replace the empty clusters and their shifts enter
+ * max_shift, without stopping the batch (km_status.repaired = 1).  Otherwise
+ * (or if a pass overflows its slots or stays short twice) empty clusters stop
+ * the batch and the caller repairs them. */
+int km_set_layout(km_ctx* ctx, const int64_t* sizes, int32_t nparts, int64_t row0, int32_t device_repair);
 /* Batches of Lloyd iterations without host synchronisation (replaces the
  * per-iteration driver round trip of kmeans_spark.py:266-313).  Between
  * km_batch_begin and km_batch_end the caller enqueues up to KM_MAX_BATCH
  * iterations, each km_assign_stats [+ its all-reduce of the stats buffer] +
- * km_update_async(tol); km_update_async also commits speculatively.  The
+ * km_update_async(tol, empty_seed) (empty_seed: int(time.time()), the seed
+ * of kmeans_spark.py:196 for an on-device repair); km_update_async also
+ * commits speculatively.  The
  * device records every iteration (status, counts) and, on convergence
  * (max_shift < tol), empty clusters or non-finite centroids, raises a gate
  * that turns the rest of the batch into no-ops.  km_batch_end synchronises
@@ -148,7 +164,7 @@ int km_update(km_ctx* ctx, km_status* st, int64_t* counts);
  * st[i], counts[i*k .. i*k+k)) and leaves the context as km_update would
  * after the last of them: km_replace_rows / km_commit apply to it. */
 int km_batch_begin(km_ctx* ctx);
-int km_update_async(km_ctx* ctx, double tol);
+int km_update_async(km_ctx* ctx, double tol, int64_t empty_seed);
 int km_batch_end(km_ctx* ctx, km_status* st, int64_t* counts, int32_t* n_ran);
 /* Empty-cluster repair (kmeans_spark.py:196-204): overwrite new centroids
  * of the given clusters with the given rows (float64 [n][d]). */

@@ -32,7 +32,7 @@ def load_golden(name):
 
 
 GOLDEN_CASES = ["test_a", "test_c", "test_d", "test_e_p3", "test_b_small", "empty", "ties",
-                "c2_small", "c3_small", "c4_small", "tight", "tight_wide"]
+                "c2_small", "c3_small", "c4_small", "tight", "tight_wide", "c5_poor"]
 
 
 @pytest.fixture(scope="session")

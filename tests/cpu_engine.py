@@ -50,7 +50,7 @@ class OracleEngine:
     def batch_begin(self):
         self._batching, self._stopped, self._slots = True, False, []
 
-    def update_async(self, tol):
+    def update_async(self, tol, empty_seed=0):
         if self._stopped:
             return
         st, counts = self.update()

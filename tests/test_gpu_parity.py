@@ -236,3 +236,74 @@ def test_tight_clusters_sse_vs_oracle(n, d, k, centers):
     np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)
     if not ref["records"][0]["empty"]:
         np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
+
+
+def test_c5_shape_poor_seeds_mass_empties_vs_oracle():
+    # c5's defining feature (BASELINE.json configs[4]) at the c5 shape: d=128,
+    # k=4096 seeded with 3 data rows + 4093 far-away points, so iteration 1
+    # leaves 4093 clusters empty and the takeSample policy
+    # (kmeans_spark.py:191-204, seed = the pinned int(time.time())) replaces
+    # them; then predict.  Checked against the oracle's restatement of the
+    # whole loop (same seed, same policy).
+    n, d, k = 12000, 128, 4096
+    X = _blobs(n, d, 64, seed=55)
+    far = np.full((k - 3, d), 100.0) + np.arange(k - 3)[:, None]
+    C0 = np.vstack([X[[0, 1, 2]], far])
+    ka = _km()
+    seed = 1700000777
+
+    class Pinned(ka.KMeans):
+        def _initialize_centroids(self, run):
+            return C0.copy()
+
+        def _empty_seed(self):
+            return seed
+
+    sc = ka.LocalContext()
+    rdd = sc.parallelize(X, 4)
+    km = Pinned(k=k, max_iter=2, tolerance=1e-12, compute_sse=True)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        km.fit(rdd, sc)
+    lines = []
+    ref = orc.lloyd_fit(X, k, 2, 1e-12, 0, True, 4, init_centroids=C0, empty_seed=lambda: seed, log=lines.append)
+    assert ref["records"][0]["empty"] and len(ref["records"][0]["empty"]) >= 4000
+    np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)
+    assert_logs_match(buf.getvalue(), "\n".join(lines) + "\n")
+    labels = km.predict(rdd, sc).to_numpy()
+    assert _check_labels(X, ref["centroids"], labels) == 0
+    assert km._runner.device_repairs >= 1   # replaced on the GPU, inside a batch
+
+
+@pytest.mark.parametrize("n,d,k,slices,seed", [
+    (200_000, 8, 300, 7, 1700000001),     # > 65536 rows: PySpark's sampler over 7 MT19937 streams
+    (90_000, 5, 40, 1, 2 ** 40 + 17),     # one partition, a seed above 2^32 (two key words)
+    (3000, 3, 2900, 3, 12345),            # ~2900 picks of 3000 rows: 4x-expectation slots, shuffle of ~3000
+])
+def test_device_empty_repair_matches_takesample_policy(n, d, k, slices, seed):
+    # far seeds empty k - 3 clusters on iteration 1; the device replaces them by
+    # takeSample(False, k - 3, seed) rows (kmeans_spark.py:191-204) inside the
+    # batch; the oracle restates PySpark's takeSample + CPython's random
+    X = _blobs(n, d, 8, seed=n + k)
+    far = np.full((k - 3, d), 100.0) + np.arange(k - 3)[:, None]
+    C0 = np.vstack([X[[0, 1, 2]], far])
+    ka = _km()
+
+    class Pinned(ka.KMeans):
+        def _initialize_centroids(self, run):
+            return C0.copy()
+
+        def _empty_seed(self):
+            return seed
+
+    sc = ka.LocalContext()
+    rdd = sc.parallelize(X, slices)
+    km = Pinned(k=k, max_iter=2, tolerance=1e-12, compute_sse=True)
+    km.verbose = False
+    km.fit(rdd, sc)
+    ref = orc.lloyd_fit(X, k, 2, 1e-12, 0, True, slices, init_centroids=C0, empty_seed=lambda: seed)
+    assert len(ref["records"][0]["empty"]) == k - 3
+    assert km._runner.device_repairs >= 1
+    np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)

@@ -15,7 +15,7 @@ from conftest import ROOT
 from oracle import kmeans_oracle as orc
 
 HEADER = os.path.join(ROOT, "include", "kmeans_amd.h")
-INJECTED = ("empty", "ties", "tight", "tight_wide")  # golden cases that inject their initial centroids
+INJECTED = ("empty", "ties", "tight", "tight_wide", "c5_poor")  # golden cases that inject their initial centroids
 
 
 def _ka():
@@ -158,7 +158,7 @@ def _fit(g, inject=True):
     return km, buf.getvalue(), np.array(km.predict(rdd, sc).collect())
 
 
-@pytest.mark.parametrize("name", ["test_a", "test_d", "empty", "ties", "test_c", "tight", "tight_wide"])
+@pytest.mark.parametrize("name", ["test_a", "test_d", "empty", "ties", "test_c", "tight", "tight_wide", "c5_poor"])
 def test_driver_reproduces_reference_with_cpu_engine(golden, cpu_engine, name):
     from test_gpu_parity import assert_logs_match
     g = golden(name)
