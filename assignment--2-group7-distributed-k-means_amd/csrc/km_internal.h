@@ -94,12 +94,15 @@ void dump_fused_stamps();  // diagnostic build only (KM_ABLATE=7)
 #endif
 // Tuning / ablation knob `name`: read from the environment only in the
 // diagnostic build (make diag, -DKM_DIAG); the product library always uses
-// `dflt`, so kernel selection depends on the geometry alone.
+// `dflt`, so kernel selection depends on the geometry alone (and, for the
+// per-key refinement in k_fused, on the last queue fraction: a cost choice
+// with no effect on results, which are exact either way).
 int diag_env(const char* name, int dflt);
 hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, const _Float16* Chi,
                         const _Float16* Clo, uint4* ChiF, uint4* CloF, const float* cn2s, const float* bnd,
                         const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,
-                        double* stats, int with_stats, int n_cu, QLayout* ql, const int* gate, hipStream_t s);
+                        double* stats, int with_stats, int refine, int n_cu, QLayout* ql, const int* gate,
+                        hipStream_t s);
 hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float* cabs, int dp, float* bnd,
                                const int* gate, hipStream_t s);
 hipError_t launch_row_norm(const float* X, const Geometry& g, float* xnorm, hipStream_t s);
@@ -125,6 +128,7 @@ hipError_t launch_update(const double* stats, const double* C64_old, const Geome
                          double* work, int64_t* counts, const uint32_t* qcount, uint32_t nq, DevStatus* status,
                          int* gate, double stop_tol, int dev_repair, hipStream_t s);
 hipError_t launch_sum_x(const float* X, const Geometry& g, double* out, hipStream_t s);
+hipError_t launch_scatter_rows(const int64_t* ids, const double* rows, int32_t n, int d, double* C, hipStream_t s);
 hipError_t launch_gather_rows(const float* X, const Geometry& g, const int64_t* idx, int32_t n, double* out,
                               hipStream_t s);
 // on-device empty-cluster repair after the update of one iteration: the

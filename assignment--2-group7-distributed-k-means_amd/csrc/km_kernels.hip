@@ -82,6 +82,57 @@ __host__ __device__ inline float screen_b0(float xn_s, float cm_s, float pm_s, i
   return fmaf(screen_slope(cm_s, dp), xn_s, screen_icpt(cm_s, pm_s, dp));
 }
 
+// Per-key screening bounds (scaled units), used where the global-cmax test
+// above cannot separate the candidates (e.g. far-away centroids inflate
+// cmax).  Every term of screen_b0 is a function of the candidate's own scaled
+// norm r (cmax -> r, the per-feature product maximum pm -> r * xabs), so a
+// centroid of norm r has screen error E(r) = e2 r^2 + e1 r + e0 for this
+// point (x = its scaled norm bound), and its exact score S = s^2(||c||^2 -
+// 2 c.x) >= r^2 - 2 r x.  For a key k (score with truncated mantissa, rho):
+//   upper(k): the centroid holding k has S <= k+ + E(R), R the largest r with
+//             r^2 - 2 r x <= k+ + E(r)   (k+ = k + rho |k|);
+//   lower(k): every centroid whose key is >= k has S >= min_r max(k- - E(r),
+//             r^2 - 2 r x): at the crossing r* >= x of the two curves, else -x^2.
+// Rounding of these fp32 evaluations is covered by explicit slack terms.
+struct KeyBounds {
+  float e2, e1, e0, x, rho;
+  __device__ __forceinline__ float upper(float k) const {
+    const float kp = k + rho * fabsf(k);
+    const float a = 1.0f - e2, b = 2.0f * x + e1;
+    const float disc = fmaxf(b * b + 4.0f * a * (e0 + kp), 0.0f);
+    const float R = (b + sqrtf(disc)) / (2.0f * a) * (1.0f + 8.0f * U24);
+    const float E = (e2 * R + e1) * R + e0;
+    return kp + E + 8.0f * U24 * (fabsf(kp) + E + R * (R + 2.0f * x));
+  }
+  __device__ __forceinline__ float lower(float k) const {
+    const float km = k - rho * fabsf(k);
+    const float a = 1.0f + e2, b = 2.0f * x - e1;
+    const float disc = b * b + 4.0f * a * (km - e0);
+    const float floor_ = -x * x * (1.0f + 8.0f * U24);
+    if (!(disc >= 0.0f)) return floor_;
+    const float r = (b + sqrtf(disc)) / (2.0f * a);
+    if (!(r >= x)) return floor_;
+    const float E = (e2 * r + e1) * r + e0;
+    const float f = km - E, g = r * (r - 2.0f * x);
+    return fmaxf(fminf(f, g) - 8.0f * U24 * (fabsf(km) + E + r * (r + 2.0f * x)), floor_);
+  }
+};
+
+// E(r) coefficients for a point of scaled norm bound xn_s (xabs_s: scaled
+// max |x_f| over the data), the terms of screen_b0 with the same 1.5 safety
+__device__ __forceinline__ KeyBounds key_bounds(float xn_s, float xabs_s, int dp, float rho) {
+  const float nm = 3.0f * (float)dp / 16.0f;
+  const float sq = sqrtf((float)dp);
+  KeyBounds kb;
+  kb.e2 = 1.5f * U24 * (1.0f + nm);
+  kb.e1 = 1.5f * ((6.5f * 2.384185791015625e-07f + 0.5f * U24 + 2.0f * nm * U24) * xn_s +
+                  28.0f * nm * U24 * fminf(xn_s, xabs_s) + 2.0f * U24 * sq);
+  kb.e0 = 1.5f * U24 * sq * xn_s;
+  kb.x = xn_s;
+  kb.rho = rho * 1.01f + 2.0f * U24;
+  return kb;
+}
+
 // ---------------------------------------------------------------------------
 // Centroid preparation: float64 centroids -> fp32 copy (direct screening),
 // bf16 hi/lo split of -2c (MFMA screening), fp32 ||c||^2, max ||c||.
@@ -720,15 +771,25 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
     // negated tests: NaN (non-finite data) falls through to the full float64
     // scan, whose np.argmin semantics then pick the first index
     uint32_t kind = 0;
+    bool same_chain = false;
     if constexpr (T2) {
       // p1, p2 in one chain (same j & 7): no certificate for the pair
-      const bool same_chain = ((p1 ^ p2) & 7u) == 0u;
+      same_chain = ((p1 ^ p2) & 7u) == 0u;
       if (!(k2 - k1 > thr2)) kind = (same_chain || !(k3 - k1 > thr3)) ? 2u : 1u;
     } else {
       if (!(k3 - k1 > thr3))
         kind = 2;
       else if (!(k2 - k1 > thr2))
         kind = 1;
+    }
+    // per-key bounds where the global test failed (wave-uniform branch)
+    if (__ballot(kind != 0u) != 0ull && kind != 0u) {
+      const KeyBounds kb = key_bounds(xn, *A.xabs * s, DP, rho);
+      const float u1 = kb.upper(k1);
+      if (u1 < kb.lower(k2))
+        kind = 0u;  // every other centroid (key >= k2) is provably worse
+      else if (kind == 2u && !same_chain && kb.lower(k3) > u1)
+        kind = 1u;  // the rest (key >= k3) is worse than i1: the answer is i1 or i2
     }
     const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
     if (h == 0 && valid) A.labels[row] = lab;
@@ -969,7 +1030,7 @@ __device__ __forceinline__ void perm_halves(uint32_t v, uint32_t& lo, uint32_t& 
 // 1 = no key updates, 2 = no MFMAs, 3 = no LDS sums, 4 = no merge / queue,
 // 5 = MFMAs + conversion + loads only, 6 = as 5 with L2-resident rows,
 // 7 = full kernel with s_memtime phase stamps, 8 = full kernel, compiler schedule
-template <int NS, int NB, bool STATS, int ABL = 0>
+template <int NS, int NB, bool STATS, int ABL = 0, bool REF = true>
 __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   constexpr int DP = 16 * NS;
@@ -1221,6 +1282,22 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
     const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k3));
     uint32_t kind = 0;
     if (!(k2 - k1 > thr2)) kind = (same_chain || !(k3 - k1 > thr3)) ? 2u : 1u;
+    // per-key bounds where the global test failed (wave-uniform branch)
+    // (REF = false: left out when the global test already settles nearly all
+    // rows, the runtime's choice from the last iteration's queue fraction)
+    float u1 = 0.0f;
+    KeyBounds kb;
+    const bool refine = REF && __ballot(kind != 0u) != 0ull;
+    if (refine) {
+      kb = key_bounds(xn * s, *A.xabs * s, DP, rho);
+      if (kind != 0u) {
+        u1 = kb.upper(k1);
+        if (u1 < kb.lower(k2))
+          kind = 0u;  // every other centroid (key >= k2) is provably worse
+        else if (kind == 2u && !same_chain && kb.lower(k3) > u1)
+          kind = 1u;  // the rest (key >= k3) is worse than i1: the answer is i1 or i2
+      }
+    }
     // p1, p2 in one chain but every other chain's best separated from k1: the
     // answer lies in that chain (j & 7 == p1 & 7), scanned exactly (kind 3,
     // k/8 centroids) instead of all k.  Rare: behind a wave-uniform branch.
@@ -1235,7 +1312,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
         if ((uint32_t)(4 + c) != cs) o = kmin(o, __uint_as_float(v1));
       }
       const float thr3x = 2.0f * B0 + rho * (fabsf(k1) + fabsf(o));
-      if (kind == 2u && same_chain && o - k1 > thr3x) kind = 3u;
+      if (kind == 2u && same_chain && (o - k1 > thr3x || (REF && kb.lower(o) > u1))) kind = 3u;
     }
     if constexpr (ABL == 7) {
       __builtin_amdgcn_sched_barrier(0);
@@ -1439,7 +1516,8 @@ bool fused_path_ok(const Geometry& g) {
 hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, const _Float16* Chi,
                         const _Float16* Clo, uint4* ChiF, uint4* CloF, const float* cn2s, const float* bnd,
                         const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,
-                        double* stats, int with_stats, int n_cu, QLayout* ql, const int* gate, hipStream_t s) {
+                        double* stats, int with_stats, int refine, int n_cu, QLayout* ql, const int* gate,
+                        hipStream_t s) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
@@ -1461,7 +1539,9 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
   const size_t lds = (size_t)g.kp * 4 + (with_stats ? (size_t)(g.dp + 1) * g.kp * 8 : 0);
 #define KM_FUSED_CASE(NS_, NB_)                                                                        \
   case NS_ * 100 + NB_:                                                                                \
-    if (with_stats)                                                                                    \
+    if (with_stats && !refine)                                                                         \
+      hipLaunchKernelGGL((k_fused<NS_, NB_, true, 0, false>), dim3(nbk), dim3(256), lds, s, a);        \
+    else if (with_stats)                                                                               \
       hipLaunchKernelGGL((k_fused<NS_, NB_, true>), dim3(nbk), dim3(256), lds, s, a);                  \
     else                                                                                               \
       hipLaunchKernelGGL((k_fused<NS_, NB_, false>), dim3(nbk), dim3(256), lds, s, a);                 \
@@ -2559,6 +2639,24 @@ __global__ void k_gather_rows(const float* __restrict__ X, int dp, int d, const 
   const int i = (int)(t / d);
   const int f = (int)(t % d);
   out[t] = (double)X[idx[i] * dp + f];
+}
+
+// Empty-cluster repair from the host (several ranks): rows[i] -> C[ids[i]]
+// in one launch
+__global__ void k_scatter_rows(const int64_t* __restrict__ ids, const double* __restrict__ rows, int32_t n, int d,
+                               double* __restrict__ C) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)n * d) return;
+  const int i = (int)(t / d);
+  const int f = (int)(t % d);
+  C[ids[i] * d + f] = rows[t];
+}
+
+hipError_t launch_scatter_rows(const int64_t* ids, const double* rows, int32_t n, int d, double* C, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t tot = (int64_t)n * d;
+  hipLaunchKernelGGL(k_scatter_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, ids, rows, n, d, C);
+  return hipGetLastError();
 }
 
 hipError_t launch_gather_rows(const float* X, const Geometry& g, const int64_t* idx, int32_t n, double* out,

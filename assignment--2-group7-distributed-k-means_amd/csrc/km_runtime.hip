@@ -73,6 +73,11 @@ struct km_ctx {
   bool have_c = false;
   int path = 0;  // 1 small, 2 mfma
   bool fused = false;  // path 2 with the fused assign + sums kernel
+  // k_fused with per-key bound refinement: on for the first iteration after
+  // new centroids, then while more than 1/64 of this rank's rows queue for
+  // exact resolution (the refinement costs ~4% where the global test settles
+  // nearly every row, and saves most of the exact work where it does not)
+  bool refine = true;
   // data
   float* X = nullptr;
   int32_t* labels = nullptr;
@@ -313,7 +318,8 @@ int run_assign(km_ctx* c, bool with_stats) {
     {
       ProfScope ps(c, KM_K_ASSIGN);
       KM_HIP(km::launch_fused(c->X, c->xnorm, g, c->Chi, c->Clo, c->ChiF, c->CloF, c->cn2s, c->bnd, c->xabs, c->cabs,
-                              c->labels, c->queue, c->qcount, c->stats, with_stats ? 1 : 0, c->n_cu, &c->ql,
+                              c->labels, c->queue, c->qcount, c->stats, with_stats ? 1 : 0, (c->refine || !with_stats) ? 1 : 0,
+                              c->n_cu, &c->ql,
                               c->gate, c->stream));
     }
     {
@@ -598,6 +604,7 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
   if (rc != KM_OK) return rc;
   KM_HIP(hipStreamSynchronize(c->stream));
   c->have_c = true;
+  c->refine = true;
   return KM_OK;
 }
 
@@ -631,6 +638,10 @@ int km_bind_stats_buffer(km_ctx* c, void* p) {
   return KM_OK;
 }
 
+static void note_queue(km_ctx* c, const km::DevStatus& s) {
+  c->refine = ((int64_t)s.q_rerank + s.q_full) * 64 > c->g.n;
+}
+
 int km_update(km_ctx* c, km_status* st, int64_t* counts) {
   KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_update: set centroids first");
   KM_REQUIRE(!c->in_batch, KM_ERR_STATE, "km_update: inside a batch (use km_update_async)");
@@ -650,6 +661,7 @@ int km_update(km_ctx* c, km_status* st, int64_t* counts) {
   }
   KM_HIP(hipStreamSynchronize(c->stream));
   const km::DevStatus& s = *c->status_host;
+  note_queue(c, s);
   if (st) {
     st->sse = s.sse;
     st->max_shift = s.max_shift;
@@ -767,6 +779,7 @@ int km_batch_end(km_ctx* c, km_status* st, int64_t* counts, int32_t* n_ran) {
     c->C64_new = c->slot_new[ran - 1];
     // the iteration that raised the gate had its own prep gated too
     c->prep_of = c->hist_host[ran - 1].stop ? nullptr : c->C64_new;
+    note_queue(c, c->hist_host[ran - 1]);
   } else if (m > 0) {
     c->C64_cur = c->slot_cur[0];
     c->C64_new = c->slot_new[0];
@@ -794,12 +807,21 @@ int km_replace_rows(km_ctx* c, const int32_t* ids, const double* rows, int32_t n
   KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_replace_rows: set centroids first");
   KM_REQUIRE(n >= 0 && (n == 0 || (ids && rows)), KM_ERR_ARG, "km_replace_rows: bad args");
   KM_HIP(hipSetDevice(c->device));
-  if (n > 0 && c->prep_of == c->C64_new) c->prep_of = nullptr;  // its images are stale now
+  if (n == 0) return KM_OK;
+  if (c->prep_of == c->C64_new) c->prep_of = nullptr;  // its images are stale now
+  c->refine = true;
+  std::vector<int64_t> ids64(n);
   for (int i = 0; i < n; ++i) {
     KM_REQUIRE(ids[i] >= 0 && ids[i] < c->g.k, KM_ERR_ARG, "km_replace_rows: cluster id out of range");
-    KM_HIP(hipMemcpyAsync(c->C64_new + (size_t)ids[i] * c->g.d, rows + (size_t)i * c->g.d,
-                          sizeof(double) * c->g.d, hipMemcpyHostToDevice, c->stream));
+    ids64[i] = ids[i];
   }
+  const int rc = ensure_scratch(c, n);
+  if (rc != KM_OK) return rc;
+  // one copy of the ids and rows, one scatter launch
+  KM_HIP(hipMemcpyAsync(c->idx_scratch, ids64.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, c->stream));
+  KM_HIP(hipMemcpyAsync(c->rows_scratch, rows, sizeof(double) * (size_t)n * c->g.d, hipMemcpyHostToDevice,
+                        c->stream));
+  KM_HIP(km::launch_scatter_rows(c->idx_scratch, c->rows_scratch, n, c->g.d, c->C64_new, c->stream));
   KM_HIP(hipStreamSynchronize(c->stream));
   return KM_OK;
 }

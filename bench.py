@@ -36,7 +36,11 @@ CONFIGS = {
     "c5": (50_000_000, 128, 4096, 4096),
     "c3_small": (4_000_000, 64, 256, 256),
     "c3_shard8": (12_500_000, 64, 256, 256),   # one GPU's share of c3 at 8 GPUs (overhead check)
+    # c5 with poor seeds (BASELINE.json configs[4]): 3 data rows + 4093 far
+    # points, so the first step replaces 4093 empty clusters (on the device)
+    "c5_poor": (50_000_000, 128, 4096, 4096),
 }
+POOR_SEEDS = {"c5_poor"}
 HBM_PEAK_GBS = 8000.0                 # MI355X spec (MI355X_MICROARCH.md)
 F16_DENSE_TFLOPS = 2516.6             # dense f16/bf16 MFMA peak (MI355X_MICROARCH.md)
 F16X3_EFFECTIVE_TFLOPS = F16_DENSE_TFLOPS / 3.0  # fp16x3 split: 3 MFMAs per product
@@ -108,6 +112,8 @@ def main():
     data = kmeans_amd.DeviceBlobs(n=N, d=d, n_centers=centers, box=10.0, std=1.0, seed=2024)
     run = km._make_runner(data, comm)
     C0 = km._initialize_centroids(run)          # takeSample policy (L72), outside the timed region
+    if args.config in POOR_SEEDS:
+        C0 = np.vstack([C0[:3], np.full((k - 3, d), 100.0) + np.arange(k - 3)[:, None]])
     eng = run.engine
     eng.set_centroids(C0)
     km.sse_history = []
@@ -189,6 +195,7 @@ def main():
                        "parallelism": f"dp{world} (rows sharded, one RCCL all-reduce of k*(d+1) f64 per step)"},
             "points_per_sec": N * it_s, "roofline": roof, "kernel_avg_ms": kernel_ms,
             "resolve": {"q_rerank": run.last["q_rerank"], "q_full": run.last["q_full"]} if run.last else None,
+            "empty_repairs_on_device": run.device_repairs,
             "arith": "fp16x3 MFMA screen with a rigorous bound, float64 exact re-rank of ambiguous points, "
                      "float64 partial sums",
         }

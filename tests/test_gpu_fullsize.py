@@ -73,3 +73,39 @@ def test_full_size_properties(N, d, k, centers, sample, chunk):
     _, mind, _ = orc.assign(np.asarray(Xs, dtype=np.float64), C0, chunk=chunk)
     est = float(np.sum(mind ** 2)) * N / sample
     assert 0.8 * est < st.sse < 1.25 * est, (st.sse, est)
+
+
+def test_full_size_c5_poor_seeds_device_repair():
+    # c5 at full size (50M x 128, k = 4096) seeded with 3 data rows + 4093 far
+    # points: one iteration empties 4093 clusters, which the device replaces
+    # inside the batch.  The replacement rows must be exactly the rows that
+    # the host restatement of takeSample(False, 4093, seed) picks
+    # (kmeans_spark.py:191-204; PySpark over the dataset's 256 partitions).
+    import kmeans_amd
+    from kmeans_amd import sampling
+    from kmeans_amd.comm import Communicator
+
+    N, d, k, seed = 50_000_000, 128, 4096, 1700000999
+
+    class Pinned(kmeans_amd.KMeans):
+        def _empty_seed(self):
+            return seed
+
+    km = Pinned(k=k, max_iter=1, tolerance=1e-12, seed=42, compute_sse=True)
+    km.verbose = False
+    data = kmeans_amd.DeviceBlobs(n=N, d=d, n_centers=k, box=10.0, std=1.0, seed=2024)
+    run = km._make_runner(data, Communicator())
+    eng = run.engine
+    C0 = np.vstack([km._initialize_centroids(run)[:3], np.full((k - 3, d), 100.0) + np.arange(k - 3)[:, None]])
+    eng.set_centroids(C0)
+    eng.set_sse(True)
+    run.run(km, None, 1)
+    assert run.device_repairs == 1
+    counts = run.last["counts"]
+    empty = np.nonzero(counts == 0)[0]
+    assert len(empty) >= 4000 and int(counts.sum()) == N
+    C1 = eng.get_centroids(0)
+    gidx = sampling.take_sample(run.pl.global_sizes, len(empty), seed)
+    np.testing.assert_array_equal(C1[empty], run.rows(gidx[:len(empty)]))
+    full = np.nonzero(counts > 0)[0]
+    assert np.all(np.isfinite(C1[full])) and np.all(np.abs(C1[full]) < 20)

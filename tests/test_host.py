@@ -42,7 +42,7 @@ def test_product_library_has_no_diagnostic_kernels():
     import subprocess
     from kmeans_amd import _lib
     syms = subprocess.run(["nm", "-C", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
-    fused = re.findall(r"k_fused<\d+, \d+, (?:true|false), (\d+)>", syms)
+    fused = re.findall(r"k_fused<\d+, \d+, (?:true|false), (\d+), (?:true|false)>", syms)
     mfma = re.findall(r"k_assign_mfma<\d+, \d+, (\d+), (?:true|false)>", syms)
     assert fused and mfma, "kernel symbols not found"
     assert set(fused) == {"0"} and set(mfma) == {"0"}, (set(fused), set(mfma))
