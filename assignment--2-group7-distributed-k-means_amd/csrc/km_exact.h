@@ -75,11 +75,16 @@ __device__ inline double np_pw(const SQ& sq, int lo, int n) {
   }
 }
 
-// np.linalg.norm of one centroid row for d <= 256 (two halvings suffice:
-// a half of n <= 256 has at most n/2 + 8 terms)
+// np.linalg.norm of one centroid row: two halvings suffice for d <= 256 (a
+// half of n <= 256 has at most n/2 + 8 terms), five for d <= 2048 (wide rows)
+template <int DEPTH, class SQ>
+__device__ inline double np_norm_d(const SQ& sq, int d) {
+  return sqrt(np_pw<DEPTH>(sq, 0, d));
+}
 template <class SQ>
 __device__ inline double np_norm(const SQ& sq, int d) {
-  return sqrt(np_pw<2>(sq, 0, d));
+  if (d <= 256) return sqrt(np_pw<2>(sq, 0, d));
+  return sqrt(np_pw<5>(sq, 0, d));
 }
 
 // same, with the point in registers (d <= DP <= 128: one block, unrolled so

@@ -821,6 +821,211 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
   }
 }
 
+// ---------------------------------------------------------------------------
+// Screening for rows wider than 256 features (kmeans_spark.py:153 takes any
+// row length), where the x tile no longer fits the registers whole.  The
+// features go in chunks of WIDE_FW = 256 (16 K-steps, the 32 rows' fp16 hi/lo
+// fragments of one chunk in 128 VGPRs), the centroids in chunks of WIDE_KC =
+// 128 (4 MFMA blocks, 64 accumulators).  For each (centroid chunk, feature
+// chunk) the workgroup stages that piece's fragments in LDS (the lane-linear
+// image of k_assign_mfma, 128 KiB) and every wave runs the 3 MFMAs per block
+// and K-step on its own 32 rows; the accumulators carry the scores across
+// feature chunks, so keys, chains, the rigorous bound and the queue are those
+// of k_assign_mfma (top-3 chains).  X is re-read once per centroid chunk
+// (from L2 for k <= 128: once).
+// ---------------------------------------------------------------------------
+static constexpr int WIDE_KC = 128, WIDE_FW = 256;
+static constexpr int WIDE_MAX_DP = 2048;  // k_fullscan stages 2 x 8 rows in LDS
+
+__global__ __launch_bounds__(256, 1) void k_assign_wide(MfmaArgs A, int dp) {
+  if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
+  constexpr int NSW = WIDE_FW / 16;  // K-steps per feature chunk
+  constexpr int NBW = WIDE_KC / 32;  // MFMA blocks per centroid chunk
+  constexpr int BLKB = NSW * 1024;   // bytes of one block's fragments (one of hi / lo)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* sHi = smem;
+  char* sLo = smem + NBW * BLKB;
+  float* sCn = reinterpret_cast<float*>(smem + 2 * NBW * BLKB);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int kp = A.kp;
+  const int64_t n = A.n;
+  const int b = ceil_log2(kp);
+  const uint32_t maskq = (1u << (b - 2)) - 1u;
+  const float s = mfma_scale(*A.xabs, *A.cabs);
+  const float cm = *A.cmax * s;
+  const float pm = (*A.cabs * s) * (*A.xabs * s) * 1.0001f;
+  const float rho = __builtin_ldexpf(1.0f, b - 2 - 23) * 1.01f;  // key truncation (relative)
+  const int nkc = (kp + WIDE_KC - 1) / WIDE_KC;
+  const int nfc = (dp + WIDE_FW - 1) / WIDE_FW;
+  const int64_t ntiles = (n + 31) / 32;
+  const int64_t nwt = (ntiles + 3) / 4;
+
+  // piece (blk, t) of centroid chunk ch / feature chunk fc at byte (blk NSW + t) KiB
+  auto stage = [&](int ch, int fc, int nb, int ns) {
+    for (int id = threadIdx.x; id < nb * NSW * 64; id += 256) {
+      const int l = id & 63;
+      const int bt = id >> 6;
+      const int blk = bt / NSW, t = bt - blk * NSW;
+      if (t >= ns) continue;
+      const size_t src = (size_t)(ch * WIDE_KC + blk * 32 + (l & 31)) * dp + fc * WIDE_FW + 16 * t + 8 * (l >> 5);
+      *reinterpret_cast<uint4*>(sHi + (size_t)id * 16) = *reinterpret_cast<const uint4*>(A.Chi + src);
+      *reinterpret_cast<uint4*>(sLo + (size_t)id * 16) = *reinterpret_cast<const uint4*>(A.Clo + src);
+    }
+    if (fc == 0)
+      for (int id = threadIdx.x; id < nb * 32; id += 256) sCn[id] = A.cn2s[(size_t)ch * WIDE_KC + id];
+  };
+
+  const uint32_t gw = blockIdx.x * 4 + wave;
+  QEntry* wq = A.queue + (size_t)gw * A.seg;
+  uint32_t qn = 0, qf = 0;
+  const char* laneHi = sHi + lane * 16;
+  const char* laneLo = sLo + lane * 16;
+  const float* laneCn = sCn + 4 * h;
+
+  // every wave of the workgroup runs the same trip counts (barriers inside);
+  // a tile past the end computes on row n - 1 and is dropped at the end
+  for (int64_t wt = blockIdx.x; wt < nwt; wt += gridDim.x) {
+    const int64_t tile = wt * 4 + wave;
+    const int64_t row = tile * 32 + r;
+    const bool valid = row < n;
+    const float* xr = A.X + (valid ? row : (n - 1)) * dp + 8 * h;
+    float a1[4], a2[4], a3[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a1[c] = a2[c] = a3[c] = FLT_MAX;
+    float xx = 0.0f;
+    for (int ch = 0; ch < nkc; ++ch) {
+      const int nb = min(WIDE_KC, kp - ch * WIDE_KC) / 32;  // 2 or 4 (kp a multiple of 64)
+      f32x16 acc[NBW];
+      for (int fc = 0; fc < nfc; ++fc) {
+        const int ns = min(WIDE_FW, dp - fc * WIDE_FW) / 16;
+        __syncthreads();  // the previous piece is consumed
+        stage(ch, fc, nb, ns);
+        __syncthreads();
+        if (fc == 0) {
+#pragma unroll
+          for (int blk = 0; blk < NBW; ++blk)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+              const float4 cv = *reinterpret_cast<const float4*>(laneCn + blk * 32 + 8 * g4);
+              acc[blk][4 * g4 + 0] = cv.x;
+              acc[blk][4 * g4 + 1] = cv.y;
+              acc[blk][4 * g4 + 2] = cv.z;
+              acc[blk][4 * g4 + 3] = cv.w;
+            }
+        }
+        // B operand: lane (r, h) holds features [16t + 8h, 16t + 8h + 8) of the chunk
+        f16x8 bh[NSW], bl[NSW];
+#pragma unroll
+        for (int t = 0; t < NSW; ++t) {
+          if (t >= ns) continue;  // (not break: the loop must unroll fully)
+          const float4 v0 = *reinterpret_cast<const float4*>(xr + fc * WIDE_FW + 16 * t);
+          const float4 v1 = *reinterpret_cast<const float4*>(xr + fc * WIDE_FW + 16 * t + 4);
+          const float xv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float xs = xv[e] * s;
+            const _Float16 hi = (_Float16)xs;
+            bh[t][e] = hi;
+            bl[t][e] = (_Float16)(xs - (float)hi);
+            if (ch == 0) xx = fmaf(xs, xs, xx);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < NSW; ++t) {
+          if (t >= ns) continue;
+#pragma unroll
+          for (int blk = 0; blk < NBW; ++blk) {
+            if (blk >= nb) continue;
+            const size_t off = (size_t)blk * BLKB + (size_t)t * 1024;
+            const f16x8 fh = *reinterpret_cast<const f16x8*>(laneHi + off);
+            const f16x8 fl = *reinterpret_cast<const f16x8*>(laneLo + off);
+            acc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh, bl[t], acc[blk], 0, 0, 0);
+            acc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fl, bh[t], acc[blk], 0, 0, 0);
+            acc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh, bh[t], acc[blk], 0, 0, 0);
+          }
+        }
+      }
+      // register reg of block blk holds centroid j = 32 (4 ch + blk) + 4h +
+      // (reg & 3) + 8 (reg >> 2); chain reg & 3 keeps j >> 2 in the key
+#pragma unroll
+      for (int blk = 0; blk < NBW; ++blk) {
+        if (blk >= nb) continue;
+        const uint32_t jq = (uint32_t)((ch * WIDE_KC) >> 2) + 8u * (uint32_t)blk + (uint32_t)h;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const float key = __uint_as_float((__float_as_uint(acc[blk][reg]) & ~maskq) | (jq | (uint32_t)(2 * (reg >> 2))));
+          top3_insert(a1[reg & 3], a2[reg & 3], a3[reg & 3], key);
+        }
+      }
+    }
+    xx += __shfl_xor(xx, 32);
+    if (tile >= ntiles) continue;
+
+    // exact merge of the 4 chains and the two lane halves (as k_assign_mfma)
+    float k1 = FLT_MAX, k2 = FLT_MAX, k3 = FLT_MAX;
+    uint32_t p1 = 0, p2 = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      top3p_insert(k1, k2, k3, p1, p2, a1[c], ((__float_as_uint(a1[c]) & maskq) << 2) | (uint32_t)c);
+      top3p_insert(k1, k2, k3, p1, p2, a2[c], ((__float_as_uint(a2[c]) & maskq) << 2) | (uint32_t)c);
+      top3p_insert(k1, k2, k3, p1, p2, a3[c], 0u);
+    }
+    {
+      const float q1 = __shfl_xor(k1, 32), q2 = __shfl_xor(k2, 32), q3 = __shfl_xor(k3, 32);
+      const uint32_t r1 = __shfl_xor(p1, 32), r2 = __shfl_xor(p2, 32);
+      top3p_insert(k1, k2, k3, p1, p2, q1, r1);
+      top3p_insert(k1, k2, k3, p1, p2, q2, r2);
+      top3p_insert(k1, k2, k3, p1, p2, q3, 0u);
+    }
+    const float xn = sqrtf(xx) * 1.0001f;
+    const float B0 = screen_b0(xn, cm, pm, dp);
+    const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k3));
+    const float thr2 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k2));
+    uint32_t kind = 0;
+    if (!(k3 - k1 > thr3))
+      kind = 2;
+    else if (!(k2 - k1 > thr2))
+      kind = 1;
+    if (__ballot(kind != 0u) != 0ull && kind != 0u) {
+      const KeyBounds kb = key_bounds(xn, *A.xabs * s, dp, rho);
+      const float u1 = kb.upper(k1);
+      if (u1 < kb.lower(k2))
+        kind = 0u;
+      else if (kind == 2u && kb.lower(k3) > u1)
+        kind = 1u;
+    }
+    const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
+    if (h == 0 && valid) A.labels[row] = lab;
+    const bool enq = (h == 0) && valid && (kind != 0);
+    const uint64_t m = __ballot(enq);
+    if (m) {
+      const uint64_t m1 = __ballot(enq && kind == 1);
+      const uint64_t m2 = m & ~m1;
+      const uint64_t below = (1ull << lane) - 1ull;
+      if (enq) {
+        QEntry q;
+        q.row = (uint32_t)row;
+        q.i1 = p1;
+        q.i2 = p2;
+        q.kind = kind;
+        const uint32_t pos = (kind == 1) ? qn + (uint32_t)__popcll(m1 & below)
+                                         : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
+        wq[pos] = q;
+      }
+      qn += (uint32_t)__popcll(m1);
+      qf += (uint32_t)__popcll(m2);
+    }
+  }
+  if (lane == 0) {
+    A.qcount[2 * gw] = qn;
+    A.qcount[2 * gw + 1] = qf;
+  }
+}
+
 static int mfma_waves_env() {
   static const int v = diag_env("KM_MFMA_WAVES", 12) == 8 ? 8 : 12;  // experiment knob: 12 (default) or 8
   return v;
@@ -839,6 +1044,8 @@ size_t queue_capacity(int64_t n, int n_cu) { return (size_t)n + (size_t)32 * 16 
 size_t qcount_words(int n_cu) { return (size_t)2 * 16 * n_cu + 16; }
 
 bool mfma_path_ok(const Geometry& g) {
+  if (g.dp > 256)  // k_assign_wide
+    return g.dp % 16 == 0 && g.dp <= WIDE_MAX_DP && g.kp >= 64 && g.kp % 64 == 0 && g.kp <= (1 << 20);
   switch (g.dp) {
     case 16: case 32: case 48: case 64: case 96: case 128: case 192: case 256:
       return g.kp >= 64 && g.kp % 64 == 0 && g.kp <= (1 << 20);
@@ -900,6 +1107,17 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
+  if (g.dp > 256) {
+    const int64_t nwt = ((g.n + 31) / 32 + 3) / 4;
+    const int nb = (int)(nwt < n_cu ? nwt : n_cu);
+    const uint32_t seg = (uint32_t)(((nwt + nb - 1) / nb) * 32);
+    ql->seg = seg;
+    ql->nwaves = (uint32_t)(nb * 4);
+    MfmaArgs a{X, g.n, g.k, g.kp, WIDE_KC, seg, Chi, Clo, cn2s, cmax, xabs, cabs, labels, queue, qcount, gate};
+    const size_t lds = 2 * (size_t)WIDE_KC * WIDE_FW * 2 + (size_t)WIDE_KC * 4;
+    hipLaunchKernelGGL(k_assign_wide, dim3(nb), dim3(256), lds, s, a, g.dp);
+    return hipGetLastError();
+  }
   int waves = 8;
   const int KC = mfma_kc(g, &waves);
   if (KC < 64) return hipErrorInvalidValue;
@@ -1665,7 +1883,8 @@ __device__ __forceinline__ uint32_t find_segment(const uint32_t* __restrict__ pr
 // global float64 atomics.  The entries of all segments are spread over all
 // waves of the grid, 8 lanes per entry (np_pw8: lane u owns NumPy's
 // accumulator u, so the rounding is the reference's), 8 entries per wave.
-__global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, int dp, int d, int k,
+template <bool WIDE>  // WIDE: d > 256 (five pairwise halvings; 512 threads, 256 VGPRs)
+__global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __restrict__ X, int dp, int d, int k,
                                                   const double* __restrict__ C64, const QEntry* __restrict__ queue,
                                                   const uint32_t* __restrict__ qcount, QLayout ql,
                                                   int32_t* __restrict__ labels, double* __restrict__ stats,
@@ -1697,12 +1916,15 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
     const double* __restrict__ ca = C64 + (size_t)a * d;
     const double* __restrict__ cb = C64 + (size_t)bb * d;
     double sa, sb;
-    np_pw8<2>([&](int f, double& ta, double& tb) {
-                const float xf = x[f];
-                ta = np_sq(ca[f], xf);
-                tb = np_sq(cb[f], xf);
-              },
-              0, d, u, sa, sb);
+    auto sq2 = [&](int f, double& ta, double& tb) {
+      const float xf = x[f];
+      ta = np_sq(ca[f], xf);
+      tb = np_sq(cb[f], xf);
+    };
+    if constexpr (WIDE)
+      np_pw8<5>(sq2, 0, d, u, sa, sb);  // d <= 2048
+    else
+      np_pw8<2>(sq2, 0, d, u, sa, sb);
     int lab = np_pick_second(sqrt(sa), sqrt(sb)) ? bb : a;
     if (!have) continue;
     if (!ok && u == 0) {
@@ -1710,7 +1932,7 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
       double best = 0.0;
       for (int j = 0; j < k; ++j) {
         const double* __restrict__ c = C64 + (size_t)j * d;
-        const double v = np_norm([&](int f) { return np_sq(c[f], x[f]); }, d);
+        const double v = np_norm_d<WIDE ? 5 : 2>([&](int f) { return np_sq(c[f], x[f]); }, d);
         if (np_better(v, best, j > 0)) {
           best = v;
           lab = j;
@@ -1779,7 +2001,7 @@ __global__ __launch_bounds__(1024) void k_rerank2(const float* __restrict__ X, i
 // each of its G points in NumPy's order (np_norm), from the chunk (one
 // conflict-free double per lane) and the point's row staged in LDS
 // (broadcast reads).  Full-scan entries sit at the back of each segment.
-template <int G>
+template <int G, bool WIDE>  // WIDE: d > 256, no LDS chunks (ch = 0)
 __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, int dp, int d, int k,
                                                    const double* __restrict__ C64T, const QEntry* __restrict__ queue,
                                                    const uint32_t* __restrict__ qcount, QLayout ql,
@@ -1811,7 +2033,7 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
       const uint32_t sg = find_segment(pre, ql.nwaves, ec);
       qe[g] = queue[(size_t)sg * ql.seg + (ql.seg - 1u - (ec - pre[sg]))];
     }
-    float xv[G][4];  // d <= 256
+    float xv[G][4];  // features [0, 256); wider rows stage the rest below
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       rows[g] = __builtin_amdgcn_readfirstlane(qe[g].row);
@@ -1827,6 +2049,10 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (lane + 64 * u < d) xs[g * d + lane + 64 * u] = xv[g][u];
+    if (WIDE)
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        for (int f = 256 + lane; f < d; f += 64) xs[g * d + f] = X[(size_t)rows[g] * dp + f];
     // np.argmin across lanes (first NaN, else smallest value, lowest index),
     // then the label and, when fused, the point's row into the sums
     auto finish = [&](int g, double bv, int bi) {
@@ -1855,7 +2081,8 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
         if (lane == 0) atomicAdd(stats + (size_t)lab * (d + 1) + d, 1.0);  // count
       }
     };
-    // chain scans (kind 3): the wave evaluates members j = chain + 8 m, lanes
+    // chain scans (kind 3, written only by the dp <= 256 screens: two pairwise
+    // halvings): the wave evaluates members j = chain + 8 m, lanes
     // over m, straight from C64T (no barriers: done before the chunk loop)
     // k <= 256: a chain has <= 32 members, so two entries share a pass (lane
     // half e of the wave on entry p + e); the other half enters the 64-lane
@@ -1872,7 +2099,7 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
         int bi = -1;
         if ((e ? a1 : a0) && j < k) {
           const float* xg = xs + (p + e) * d;
-          bv = np_norm([&](int f) { return np_sq(C64T[(size_t)f * k + j], xg[f]); }, d);
+          bv = np_norm_d<2>([&](int f) { return np_sq(C64T[(size_t)f * k + j], xg[f]); }, d);
           bi = j;
         }
         if (a0) {
@@ -1892,7 +2119,7 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
       int bi = -1;
       for (int j = chain[g] + 8 * lane; j < k; j += 8 * 64) {
         const float* xg = xs + g * d;
-        const double v = np_norm([&](int f) { return np_sq(C64T[(size_t)f * k + j], xg[f]); }, d);
+        const double v = np_norm_d<2>([&](int f) { return np_sq(C64T[(size_t)f * k + j], xg[f]); }, d);
         if (np_better(v, bv, bi >= 0)) {
           bv = v;
           bi = j;
@@ -1913,7 +2140,27 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
     // most batches hold chain scans only: skip the chunk pass unless some
     // wave of the workgroup still has a full scan
     if (!__syncthreads_or(any_full)) continue;
-    for (int c0 = 0; c0 < k; c0 += ch) {
+    if constexpr (WIDE) {
+      // wide rows (no LDS room for a chunk): lane j reads C64T straight
+      // from L2, consecutive centroids on consecutive lanes
+      static_assert(G == 2 || G == 4, "entries per wave");
+      auto direct = [&](int j, const float* xg, double& bst, int& bjj) {
+        const double v = np_norm_d<5>([&](int f) { return np_sq(C64T[(size_t)f * k + j], xg[f]); }, d);
+        if (np_better(v, bst, bjj >= 0)) {
+          bst = v;
+          bjj = j;
+        }
+      };
+      for (int j = lane; j < k; j += 64) {
+        if (have[0]) direct(j, xs, best[0], bj[0]);
+        if (have[1]) direct(j, xs + d, best[1], bj[1]);
+        if constexpr (G == 4) {
+          if (have[2]) direct(j, xs + 2 * d, best[2], bj[2]);
+          if (have[3]) direct(j, xs + 3 * d, best[3], bj[3]);
+        }
+      }
+    }
+    for (int c0 = 0; !WIDE && c0 < k; c0 += ch) {
       __syncthreads();  // the previous chunk is consumed (and the rows staged)
       const int cw = min(ch, k - c0);
       for (int i = threadIdx.x; i < d * ch; i += blockDim.x) {
@@ -1928,7 +2175,7 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
         for (int g = 0; g < G; ++g) {
           if (!have[g]) continue;
           const float* xg = xs + g * d;
-          const double v = np_norm([&](int f) { return np_sq(ct[(size_t)f * ch], xg[f]); }, d);
+          const double v = np_norm_d<2>([&](int f) { return np_sq(ct[(size_t)f * ch], xg[f]); }, d);
           if (np_better(v, best[g], bj[g] >= 0)) {
             best[g] = v;
             bj[g] = c0 + lane;
@@ -1949,30 +2196,37 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   constexpr size_t LDS_MAX = 160 * 1024;
   const size_t pre_bytes = ((size_t)ql.nwaves + 1) * 4;
   if (pre_bytes > LDS_MAX / 4) return hipErrorInvalidValue;
-  if (g.d > 256) return hipErrorInvalidValue;
+  if (g.d > WIDE_MAX_DP) return hipErrorInvalidValue;
   // full / chain scans first (labels only); k_rerank2 then adds the sums of
   // both queues through its LDS table
   static const int fs_g = diag_env("KM_FS_G", 2);  // entries per wave: 2 or 4
   const int G = fs_g == 4 ? 4 : 2;
-  const int ch = g.d <= 128 ? 64 : 32;  // chunk columns: <= 64 KiB of LDS
+  const int ch = g.d <= 128 ? 64 : (g.d <= 256 ? 32 : 0);  // chunk columns (<= 64 KiB of LDS); 0: direct
   const size_t fs_lds = (size_t)g.d * ch * 8 + (size_t)8 * G * g.d * 4 + pre_bytes;
   if (fs_lds > LDS_MAX) return hipErrorInvalidValue;
   static const int use_chain = diag_env("KM_CHAIN", 1);
   static const int pair_chain = diag_env("KM_PAIR_CHAIN", 1);
   static const int fs_wg = diag_env("KM_FS_WG", 1);  // workgroups per CU (3: no measurable change)
-  if (G == 4)
-    hipLaunchKernelGGL(k_fullscan<4>, dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T, queue,
-                       qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, gate);
+  if (ch == 0)
+    hipLaunchKernelGGL((k_fullscan<2, true>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
+                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, gate);
+  else if (G == 4)
+    hipLaunchKernelGGL((k_fullscan<4, false>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
+                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, gate);
   else
-    hipLaunchKernelGGL(k_fullscan<2>, dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T, queue,
-                       qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, gate);
+    hipLaunchKernelGGL((k_fullscan<2, false>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
+                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, gate);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t tab_bytes = (size_t)(g.d + 1) * g.kp * 8;
   const size_t pres = (stats ? 2 : 1) * pre_bytes;
   const int tab_kp = (stats && tab_bytes + pres <= LDS_MAX) ? g.kp : 0;
-  hipLaunchKernelGGL(k_rerank2, dim3(n_cu), dim3(1024), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d, g.k,
-                     C64, queue, qcount, ql, labels, stats, tab_kp, gate);
+  if (g.d > 256)
+    hipLaunchKernelGGL(k_rerank2<true>, dim3(n_cu), dim3(512), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
+                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, gate);
+  else
+    hipLaunchKernelGGL(k_rerank2<false>, dim3(n_cu), dim3(1024), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
+                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, gate);
   return hipGetLastError();
 }
 
@@ -2015,6 +2269,9 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
   const int P = 64 / L;        // rows per load instruction (L <= 64)
   const int q = lane / L;
   const int mm = lane % L;
+  // L not dividing 64 (fr = 48, 96, 152, 196, ...): the lanes past the last
+  // whole row idle (lane q = P would repeat row u + 1's first features)
+  const bool act = q < P;
   constexpr int U = 8;         // float4 loads in flight per lane
   for (int64_t cr = r0 + (int64_t)wave * 64; cr < r1; cr += (int64_t)nwaves * 64) {
     const int nrow = (int)min((int64_t)64, r1 - cr);
@@ -2026,14 +2283,14 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int rr = rb + u * P + q;
-        v[u] = rr < nrow ? *reinterpret_cast<const float4*>(base + (size_t)rr * dp + 4 * mm)
-                         : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[u] = (act && rr < nrow) ? *reinterpret_cast<const float4*>(base + (size_t)rr * dp + 4 * mm)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int rr = rb + u * P + q;
         const int lab = __shfl(labreg, rr & 63);
-        if (rr < nrow && lab >= c0 && lab < c1) {
+        if (act && rr < nrow && lab >= c0 && lab < c1) {
           double* t = tab + (lab - c0) * RS + mm;
           atomicAdd(t, (double)v[u].x);
           atomicAdd(t + L, (double)v[u].y);
@@ -2065,6 +2322,23 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
 // those needing the fewest cluster ranges; segments stay >= 64 bytes
 static void stats_ranges(const Geometry& g, int* fr_out, int* kr_out) {
   int best_fr = g.dp, best_kr = 0, best_ncr = 1 << 30;
+  if (g.dp > 256) {
+    // wide rows: any multiple of 4 dividing dp, at most 256 (dp = 2000: 80)
+    for (int fr = 256; fr >= 16; fr -= 4) {
+      if (g.dp % fr) continue;
+      int kr = (int)(STATS_LDS / ((size_t)(fr + 1) * 8));
+      if (kr > g.k) kr = g.k;
+      const int ncr = (g.k + kr - 1) / kr;
+      if (ncr < best_ncr) {
+        best_ncr = ncr;
+        best_fr = fr;
+        best_kr = kr;
+      }
+    }
+    *fr_out = best_fr;
+    *kr_out = best_kr;
+    return;
+  }
   for (int fr = g.dp; fr >= 16 && g.dp % fr == 0 && fr % 4 == 0; fr /= 2) {
     int kr = (int)(STATS_LDS / ((size_t)(fr + 1) * 8));
     if (kr > g.k) kr = g.k;
@@ -2083,7 +2357,7 @@ static void stats_ranges(const Geometry& g, int* fr_out, int* kr_out) {
 hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels, double* stats, int n_cu,
                         const int* gate, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
-  if (g.dp > 256 || g.dp % 4) return hipErrorInvalidValue;
+  if (g.dp > WIDE_MAX_DP || g.dp % 4) return hipErrorInvalidValue;
   int fr = 0, kr = 0;
   stats_ranges(g, &fr, &kr);
   if (kr < 1) return hipErrorInvalidValue;
@@ -2315,9 +2589,44 @@ __global__ __launch_bounds__(256) void k_sse(const float* __restrict__ X, int64_
   if (lane == 0 && ss != 0.0) atomicAdd(sse, ss);
 }
 
+// rows wider than 256 features: one row per wave, lanes over float4 slots
+__global__ __launch_bounds__(256) void k_sse_wide(const float* __restrict__ X, int64_t n, int dp,
+                                                  const int32_t* __restrict__ labels, const double* __restrict__ C64P,
+                                                  double* __restrict__ sse, const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  double ss = 0.0;
+  for (int64_t row = gw; row < n; row += nw) {
+    const int lb = labels[row];
+    const float* x = X + (size_t)row * dp;
+    const double* c = C64P + (size_t)lb * dp;
+    for (int f = 4 * lane; f < dp; f += 256) {
+      const float4 v = *reinterpret_cast<const float4*>(x + f);
+      const double2 ca = *reinterpret_cast<const double2*>(c + f);
+      const double2 cb = *reinterpret_cast<const double2*>(c + f + 2);
+      const double t0 = (double)v.x - ca.x, t1 = (double)v.y - ca.y;
+      const double t2 = (double)v.z - cb.x, t3 = (double)v.w - cb.y;
+      ss = fma(t0, t0, ss);
+      ss = fma(t1, t1, ss);
+      ss = fma(t2, t2, ss);
+      ss = fma(t3, t3, ss);
+    }
+  }
+  ss = wave_sum(ss);
+  if (lane == 0 && ss != 0.0) atomicAdd(sse, ss);
+}
+
 hipError_t launch_sse(const float* X, const Geometry& g, const int32_t* labels, const double* C64P, double* sse,
                       const int* gate, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
+  if (g.dp > 256) {
+    int64_t blocks = (g.n + 3) / 4;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_sse_wide, dim3((unsigned)blocks), dim3(256), 0, s, X, g.n, g.dp, labels, C64P, sse, gate);
+    return hipGetLastError();
+  }
   const int L = g.dp / 4;
   const int P = 64 / L;
   int64_t blocks = (g.n + 4 * P * 4 - 1) / (4 * P * 4);  // 4 waves per block, P*4 rows per wave-step
@@ -2352,6 +2661,7 @@ size_t sorted_stats_words(int64_t n, int k) { return 2 * (size_t)n + 3 * (size_t
 // is cheaper
 bool stats_needs_sort(const Geometry& g) {
   static const int min_ranges = diag_env("KM_SORT_MIN_RANGES", 3);  // A/B knob
+  if (g.dp > 256) return false;  // k_segsum holds a row in one wave-instruction
   int fr = 0, kr = 0;
   stats_ranges(g, &fr, &kr);
   return kr == 0 || (g.k + kr - 1) / kr >= min_ranges;

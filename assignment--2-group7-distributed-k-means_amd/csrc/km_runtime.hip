@@ -620,7 +620,7 @@ int km_get_centroids(km_ctx* c, int32_t which, double* out) {
 int km_assign_stats(km_ctx* c) {
   KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_assign_stats: set centroids first");
   KM_REQUIRE(c->path != 0, KM_ERR_UNSUPPORTED,
-             "km_assign_stats: no kernel for d=" + std::to_string(c->g.d) + " (supported: d <= 256)");
+             "km_assign_stats: no kernel for d=" + std::to_string(c->g.d) + " (supported: d <= 2048)");
   KM_HIP(hipSetDevice(c->device));
   return run_assign(c, true);
 }

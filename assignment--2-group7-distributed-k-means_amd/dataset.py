@@ -12,15 +12,29 @@ The reference receives a PySpark RDD of ``(d,)`` float arrays built by
   HBM (benchmarks; nothing on the host).
 
 ``place`` turns one into a ``Placement``: the global partition layout (needed
-by the takeSample policy), this rank's contiguous block of partitions and
-rows, and how to fetch rows by global index.  With W ranks, rank r owns
-partitions ``[r*P//W, (r+1)*P//W)`` (an array input is cut into W row blocks),
-so concatenating the ranks' predictions restores input order.
+by the takeSample policy) and this rank's contiguous block of partitions and
+rows.  With W ranks, rank r owns partitions ``[r*P//W, (r+1)*P//W)`` (a
+one-partition input is cut into W row blocks), so concatenating the ranks'
+predictions restores input order.
+
+Ingestion is sharded at the source: the layout comes from a count pass
+(for a PySpark RDD it runs on the executors: one ``(rows, width, dtype)``
+triple per partition reaches the rank), and each rank then materialises only
+its own partitions (``mapPartitionsWithIndex`` filtered to its block), so no
+rank holds another rank's rows.  Rows needed by index later (takeSample
+picks, kmeans_spark.py:72, 196) are gathered from the ranks' HBM
+(``LloydRunner.rows``).
+
+Rows are stored in HBM as float32 (the compute contract, see ``KMeans``): a
+float64 input is rounded once at load, and every row the framework uses
+afterwards -- assignment, sums, initial and replacement centroids -- is that
+rounded row.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
-from typing import Any, List, Optional, Sequence
+import itertools
+from dataclasses import dataclass
+from typing import Any, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -55,15 +69,23 @@ class LocalRDD:
     def glom(self):
         return LocalRDD([[list(p)] for p in self._parts], self.ctx)
 
-    def partition_arrays(self) -> List[np.ndarray]:
-        out = []
-        for p in self._parts:
-            if isinstance(p, np.ndarray) and p.ndim == 2:
-                out.append(p)
-            else:
-                items = list(p)
-                out.append(np.asarray(items) if items else None)
-        return out
+    def partition_len(self, i: int) -> int:
+        return len(self._parts[i])
+
+    def partition_array(self, i: int) -> Optional[np.ndarray]:
+        """Partition i as a 2-D array (None when empty); only this rank's
+        partitions are ever materialised (``place``)."""
+        p = self._parts[i]
+        if isinstance(p, np.ndarray) and p.ndim == 2:
+            return p if len(p) else None
+        items = list(p)
+        return np.asarray(items) if items else None
+
+    def partition_arrays(self) -> List[Optional[np.ndarray]]:
+        return [self.partition_array(i) for i in range(len(self._parts))]
+
+    def mapPartitionsWithIndex(self, f) -> "LocalRDD":
+        return LocalRDD([list(f(i, iter(p))) for i, p in enumerate(self._parts)], self.ctx)
 
     def collect(self) -> list:
         out = []
@@ -137,40 +159,75 @@ class DeviceBlobs:
 @dataclass
 class Placement:
     global_sizes: List[int]          # rows per global partition (takeSample layout)
-    local_rows: Optional[np.ndarray]  # this rank's rows (host), None for DeviceBlobs
+    local_rows: Optional[np.ndarray]  # this rank's rows (host, only its own), None for DeviceBlobs
     row0: int                        # global index of this rank's first row
     n_local: int
     n_global: int
     d: int
     dtype: Any
-    host_partitions: Optional[List[np.ndarray]] = field(default=None, repr=False)
     blobs: Optional[DeviceBlobs] = None
 
-    def host_rows(self, gidx: Sequence[int]) -> Optional[np.ndarray]:
-        """Rows by global index when every rank holds the data on the host."""
-        if self.host_partitions is None:
-            return None
-        starts = np.cumsum([0] + [len(p) if p is not None else 0 for p in self.host_partitions])
-        out = []
-        for g in gidx:
-            pi = int(np.searchsorted(starts, g, side="right") - 1)
-            out.append(self.host_partitions[pi][g - starts[pi]])
-        return np.asarray(out, dtype=self.dtype).reshape(len(out), self.d)
+
+def _count_width(it):
+    """Per partition, on the executors: (rows, row width, dtype) -- no rows leave."""
+    n, width, kind = 0, -1, ""
+    for row in it:
+        if n == 0:
+            a = np.asarray(row)
+            width, kind = int(a.size), a.dtype.str
+        n += 1
+    yield n, width, kind
 
 
-def _partitions_of(rdd) -> List[np.ndarray]:
+def _layout(rdd) -> Tuple[List[int], Optional[int], Any]:
+    """Global partition sizes, row width and dtype, without moving rows."""
     if isinstance(rdd, np.ndarray):
         if rdd.ndim != 2:
             raise ValueError("input array must be 2-D [n][d]")
-        return [rdd]
+        return [rdd.shape[0]], (rdd.shape[1] if rdd.shape[0] else None), rdd.dtype
     if isinstance(rdd, LocalRDD):
-        parts = rdd.partition_arrays()
-    elif hasattr(rdd, "glom"):  # PySpark RDD (duck-typed)
-        parts = [np.asarray(p) if len(p) else None for p in rdd.glom().collect()]
+        sizes = [rdd.partition_len(i) for i in range(rdd.getNumPartitions())]
+        for i, n in enumerate(sizes):
+            if n:
+                p = rdd._parts[i]
+                first = np.asarray(p[0])
+                return sizes, int(first.size), (p.dtype if isinstance(p, np.ndarray) else first.dtype)
+        return sizes, None, np.float64
+    if hasattr(rdd, "mapPartitions"):  # PySpark RDD (duck-typed)
+        trip = rdd.mapPartitions(_count_width).collect()
+        sizes = [int(t[0]) for t in trip]
+        for n, width, kind in trip:
+            if n:
+                return sizes, int(width), np.dtype(kind)
+        return sizes, None, np.float64
+    raise TypeError(f"unsupported dataset type {type(rdd).__name__}: expected an RDD, LocalRDD, "
+                    f"ndarray or DeviceBlobs")
+
+
+def _own_rows(rdd, lo: int, hi: int, d: int, row_range: Optional[Tuple[int, int]] = None) -> np.ndarray:
+    """This rank's rows: partitions [lo, hi), or rows [a, b) of the single
+    partition 0 (row_range).  Only they are materialised / transferred."""
+    if isinstance(rdd, np.ndarray):
+        a, b = row_range if row_range else (0, rdd.shape[0])
+        return rdd[a:b]
+    if isinstance(rdd, LocalRDD):
+        if row_range:
+            p = rdd.partition_array(0)
+            return p[row_range[0]:row_range[1]] if p is not None else np.zeros((0, d))
+        mine = [rdd.partition_array(i) for i in range(lo, hi)]
+        mine = [m.reshape(len(m), d) for m in mine if m is not None]
+        return np.concatenate(mine) if mine else np.zeros((0, d))
+
+    if row_range:
+        a, b = row_range
+
+        def keep(i, it):
+            return itertools.islice(it, a, b) if i == 0 else iter(())
     else:
-        raise TypeError(f"unsupported dataset type {type(rdd).__name__}: expected an RDD, LocalRDD, "
-                        f"ndarray or DeviceBlobs")
-    return parts
+        def keep(i, it):
+            return it if lo <= i < hi else iter(())
+    rows = rdd.mapPartitionsWithIndex(keep).collect()
+    return np.asarray(rows).reshape(len(rows), d) if rows else np.zeros((0, d))
 
 
 def place(rdd, comm) -> Placement:
@@ -182,39 +239,24 @@ def place(rdd, comm) -> Placement:
         layout = [((i + 1) * rdd.n) // P - (i * rdd.n) // P for i in range(P)]
         return Placement(global_sizes=layout, local_rows=None, row0=row0, n_local=sizes[r], n_global=rdd.n,
                          d=rdd.d, dtype=np.float64, blobs=rdd)
-    parts = _partitions_of(rdd)
-    d = None
-    dtype = None
-    for p in parts:
-        if p is not None and p.size:
-            if p.ndim != 2:
-                p = p.reshape(len(p), -1)
-            d = p.shape[1]
-            dtype = p.dtype
-            break
+    sizes, d, dtype = _layout(rdd)
     if d is None:
         raise ValueError("Not enough data points (0) to initialize clusters")
-    parts = [None if p is None else np.asarray(p).reshape(len(p), d) for p in parts]
-    if not np.issubdtype(dtype, np.floating):
+    if not np.issubdtype(np.dtype(dtype), np.floating):
         dtype = np.float64
-    sizes = [0 if p is None else len(p) for p in parts]
     W, r = comm.world, comm.rank
-    if len(parts) == 1 and W > 1:
-        # a single array: cut it into W row blocks
-        X = parts[0]
-        n = len(X)
-        parts = [X[(i * n) // W:((i + 1) * n) // W] for i in range(W)]
-        mine = [parts[r]]
-        row0 = (r * n) // W
-        global_sizes = sizes  # the takeSample layout is still ONE partition
-        host_parts = [X]
+    if len(sizes) == 1 and W > 1:
+        # one partition: cut into W row blocks (the takeSample layout is still ONE partition)
+        n = sizes[0]
+        a, b = (r * n) // W, ((r + 1) * n) // W
+        local = _own_rows(rdd, 0, 1, d, row_range=(a, b))
+        row0 = a
     else:
-        P = len(parts)
+        P = len(sizes)
         lo, hi = (r * P) // W, ((r + 1) * P) // W
-        mine = [p for p in parts[lo:hi] if p is not None]
+        local = _own_rows(rdd, lo, hi, d)
         row0 = int(sum(sizes[:lo]))
-        global_sizes = sizes
-        host_parts = parts
-    local = np.concatenate(mine) if mine else np.zeros((0, d))
-    return Placement(global_sizes=global_sizes, local_rows=local, row0=row0, n_local=len(local),
-                     n_global=int(sum(sizes)), d=d, dtype=dtype, host_partitions=host_parts)
+    if local.ndim != 2:
+        local = local.reshape(len(local), d)
+    return Placement(global_sizes=sizes, local_rows=local, row0=row0, n_local=len(local),
+                     n_global=int(sum(sizes)), d=d, dtype=np.dtype(dtype))

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import sys
 import time
+import weakref
 from typing import List, Optional
 
 import numpy as np
@@ -59,10 +60,9 @@ class LloydRunner:
             self.engine.set_layout(pl.global_sizes, 0, True)
 
     def rows(self, gidx: List[int]) -> np.ndarray:
-        """Rows by global index (what ``rdd.takeSample`` returns, L72/L196)."""
-        host = self.pl.host_rows(gidx)
-        if host is not None:
-            return host
+        """Rows by global index (what ``rdd.takeSample`` returns, L72/L196):
+        each rank gathers the ones it holds from HBM (the stored float32 rows,
+        as float64), one sum all-reduce assembles them (others contribute 0)."""
         gidx = np.asarray(gidx, dtype=np.int64)
         lo, hi = self.pl.row0, self.pl.row0 + self.pl.n_local
         mine = np.nonzero((gidx >= lo) & (gidx < hi))[0]
@@ -211,6 +211,21 @@ class LabelsRDD(LocalRDD):
         return self._gather()
 
 
+def _ref_to(obj):
+    """A reference to the fitted dataset for predict's reuse test: weak where
+    the type allows (the model does not keep the host data alive), else the
+    object itself.  Compared by identity (``is``), never by ``id()``, which
+    CPython reuses after garbage collection."""
+    try:
+        return weakref.ref(obj)
+    except TypeError:
+        return lambda: obj
+
+
+def _deref(ref):
+    return ref() if ref is not None else None
+
+
 class KMeans:
     """Distributed K-Means, MI355X-native (kmeans_spark.py:19-47).
 
@@ -231,7 +246,7 @@ class KMeans:
         self._validate_parameters()
         self.iterations_run = 0  # kept as the reference leaves it (never updated, L47)
         self._runner: Optional[LloydRunner] = None
-        self._runner_key = None
+        self._runner_src = None  # the fitted dataset (weak reference where the type allows)
         self.verbose = True
 
     def _validate_parameters(self):
@@ -280,7 +295,7 @@ class KMeans:
             rdd.cache()                                        # L256
         comm = Communicator()
         run = self._make_runner(rdd, comm)
-        self._runner, self._runner_key = run, id(rdd)
+        self._runner, self._runner_src = run, _ref_to(rdd)
         self.centroids = self._initialize_centroids(run)       # L259
         self.sse_history = []                                  # L260
         say = self._log(comm)
@@ -300,8 +315,8 @@ class KMeans:
         if self.centroids is None:
             raise ValueError("Model must be fitted before prediction")
         comm = Communicator()
-        if self._runner is not None and self._runner_key == id(rdd):
-            run = self._runner
+        if self._runner is not None and _deref(self._runner_src) is rdd:
+            run = self._runner  # the rows are resident from fit
         else:
             run = self._make_runner(rdd, comm)
         run.engine.set_centroids(np.asarray(self.centroids, dtype=np.float64))

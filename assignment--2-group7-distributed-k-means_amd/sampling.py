@@ -116,8 +116,12 @@ def _bernoulli_pass(partition_sizes: Sequence[int], fraction: float, seed: int, 
     rank = comm.rank if comm is not None else 0
     mine = [p for p in range(len(partition_sizes)) if p % world == rank and partition_sizes[p] > 0]
     parts = None
-    if device is not None and mine:
-        picks = device(np.array([seed ^ p for p in mine], dtype=np.uint64),
+    # the streams' MT keys: random.Random(seed ^ p) seeds with abs(seed ^ p)
+    # (negative seeds are valid); the device pass takes 64-bit keys, larger
+    # ones stay on the host path
+    keys = [abs(int(seed) ^ p) for p in mine]
+    if device is not None and mine and max(keys) < 2 ** 64:
+        picks = device(np.array(keys, dtype=np.uint64),
                        np.array([partition_sizes[p] for p in mine], dtype=np.int64), bases[mine], fraction)
         parts = None if picks is None else [picks]
     if parts is None and len(mine) > 1:

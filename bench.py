@@ -76,14 +76,44 @@ def init_dist(args):
     return world, rank, local
 
 
+def usable_cpus():
+    """os.cpu_count(), capped by this process's CPU
+    affinity and cgroup quota: on the GPU box os.cpu_count() reports the whole
+    host while a job gets a share of it."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(d, k, n_total, seconds):
     """The reference closure restated (oracle, per-point np.linalg.norm +
-    argmin + dict combine; kmeans_spark.py:147-173) on a bounded sample, one
-    process per worker, like Spark local[N]."""
+    argmin + reduceByKey combine; kmeans_spark.py:147-173) on a bounded
+    sample, one process per usable CPU, like Spark local[*].  Cross-checked
+    against the reference's own closures by scripts/check_cpu_baseline.py
+    (within 10 %, profiles/r2_cpu_baseline_check.txt)."""
     from multiprocessing import get_context
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cpu_baseline as cb
-    workers = max(1, min(16, os.cpu_count() or 1))
+    workers = usable_cpus()
     # calibrate points per worker for ~`seconds` of work
     rate = cb.calibrate(d, k)
     per = int(max(2000, min(400_000, rate * seconds)))
@@ -94,7 +124,7 @@ def cpu_baseline(d, k, n_total, seconds):
     pts = sum(r[0] for r in res)
     pps = pts / dt
     return {"value": pps / n_total, "unit": f"Lloyd it/s (extrapolated to N={n_total:,})", "cores": workers,
-            "kind": "port", "points_per_sec": pps,
+            "kind": "port", "points_per_sec": pps, "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
             "sample": f"{workers} workers x {per} points, d={d}, k={k}, one assign+combine pass each "
                       f"(oracle/cpu_baseline.py restating kmeans_spark.py:147-173); it/s = points/s / N"}
 

@@ -22,28 +22,41 @@ def _sample(d, k, n, seed):
     return X, C
 
 
-def _partition_pass(X, C):
-    acc = {}
-    for point in X:
+def _assign(part, C):
+    for point in part:
         dist = np.linalg.norm(C - point, axis=1)      # L153
-        cid = int(np.argmin(dist))                    # L156
-        if cid in acc:                                # reduceByKey lambda, L169-171
-            s, c = acc[cid]
-            acc[cid] = (s + point, c + 1)
-        else:
-            acc[cid] = (point, 1)
+        yield int(np.argmin(dist)), (point, 1)        # L156-159
+
+
+def _merge(a, b):                                     # reduceByKey lambda, L169-171
+    return a[0] + b[0], a[1] + b[1]
+
+
+def _partition_pass(X, C):
+    # map-side combine of reduceByKey over the streamed (cid, (point, 1)) pairs
+    acc = {}
+    for cid, val in _assign(X, C):
+        acc[cid] = _merge(acc[cid], val) if cid in acc else val
     return acc
+
+
+def _cached_rows(X):
+    # a cached partition holds its rows as Python objects (rdd.cache(), L256):
+    # the per-point views exist before the pass, as in the PySpark stand-in
+    return list(X)
 
 
 def calibrate(d, k, n=2000):
     X, C = _sample(d, k, n, 0)
+    rows = _cached_rows(X)
     t0 = time.perf_counter()
-    _partition_pass(X, C)
+    _partition_pass(rows, C)
     return n / (time.perf_counter() - t0)
 
 
 def run_partition(d, k, n, seed):
     X, C = _sample(d, k, n, seed + 1)
+    rows = _cached_rows(X)
     t0 = time.perf_counter()
-    _partition_pass(X, C)
+    _partition_pass(rows, C)
     return n, time.perf_counter() - t0

@@ -135,6 +135,12 @@ def _check_labels(X, C, labels):
     (1000, 40, 70, 10),        # d=40 -> 48 padded (fused <3,4>, generic row norms)
     (5000, 64, 300, 60),       # k=300 -> kp=320: unfused MFMA path + LDS-range statistics
     (6000, 128, 1200, 100),    # statistics tiled over 2 cluster ranges x 8 feature ranges
+    (4000, 40, 300, 30),       # dp 48 unfused: k_stats lane groups of 12 (4 lanes idle)
+    (4000, 90, 200, 30),       # dp 96 unfused: lane groups of 24
+    (3000, 180, 150, 30),      # dp 192 unfused: lane groups of 48
+    (6000, 300, 70, 20),       # d=300 -> 304: feature-chunked screen (k_assign_wide), one centroid chunk
+    (3000, 784, 200, 40),      # d=784: 2 centroid x 4 feature chunks, statistics over 196-wide ranges
+    (2000, 300, 700, 50),      # wide rows, 6 centroid chunks, 3 cluster ranges
 ])
 def test_one_step_vs_oracle(n, d, k, centers):
     X = _blobs(n, d, centers, seed=n + d + k)
@@ -199,6 +205,8 @@ def test_predict_requires_fit():
     (8000, 32, 264, 264),    # unfused, top-2 chains, duplicates on the same chain -> full scans
     (6000, 200, 40, 40),     # d = 200: pairwise split 96 + 104
     (6000, 250, 20, 20),     # d = 250: split 120 + (64 + 66), two levels
+    (3000, 300, 40, 40),     # d = 300: wide re-rank (k_rerank2<true>), three levels
+    (2000, 784, 24, 24),     # d = 784: 392 + 392 -> ... five levels
 ])
 def test_near_ties_one_ulp_apart_vs_oracle(n, d, nb, off):
     # centroids duplicated and nudged by one float64 ulp: every point is a
@@ -212,6 +220,22 @@ def test_near_ties_one_ulp_apart_vs_oracle(n, d, nb, off):
     labels = _one_step(X, C0, iters=1)._runner.engine.labels()
     lab_ref = orc.assign(X, C0)[0]
     np.testing.assert_array_equal(labels, lab_ref)
+
+
+@pytest.mark.parametrize("n,d,nb", [(3000, 300, 30), (1500, 784, 16), (1200, 2000, 8)])
+def test_wide_rows_triple_ties_full_scan_vs_oracle(n, d, nb):
+    # three centroids one float64 ulp apart: no re-rank certificate, so the
+    # points go to the wide full scan (k_fullscan<2, true>, C64T from L2);
+    # labels must be np.argmin over np.linalg.norm bit for bit
+    X = _blobs(n, d, 16, 29 + d)
+    base = X[np.random.default_rng(d).choice(n, nb, replace=False)]
+    up = np.nextafter(base, np.inf)
+    C0 = np.concatenate([base, up, np.nextafter(up, np.inf)])
+    km = _one_step(X, C0, iters=1)
+    lab_ref = orc.assign(X, C0)[0]
+    np.testing.assert_array_equal(km._runner.engine.labels(), lab_ref)
+    ref = orc.lloyd_fit(X, len(C0), 1, 1e-12, 0, True, 1, init_centroids=C0)
+    np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)
 
 
 @pytest.mark.parametrize("n,d,k,centers", [

@@ -37,7 +37,7 @@ def test_device_bernoulli_equals_host(engine, sizes, fraction, seed):
 def test_take_sample_with_device_pass(engine):
     from kmeans_amd import sampling
     sizes = [300_000, 200_001, 0, 150_000]
-    for num, seed in [(7, 42), (256, 1_699_999_999), (1, 3)]:
+    for num, seed in [(7, 42), (256, 1_699_999_999), (1, 3), (5, -987654321), (9, -(2 ** 63)), (4, 2 ** 64 + 5)]:
         assert sampling.take_sample(sizes, num, seed, device=engine.bernoulli) == \
             sampling.take_sample(sizes, num, seed)
 

@@ -70,6 +70,33 @@ def test_take_sample_matches_oracle_restatement(sizes, num, seed):
     assert sampling.take_sample(sizes, num, seed) == orc.take_sample_indices(sizes, num, seed)
 
 
+def test_device_pass_keys_for_negative_and_huge_seeds():
+    # the device pass gets abs(seed ^ p) as a uint64 MT key (what
+    # random.Random(seed ^ p) seeds with); keys of 2^64 and more stay on the
+    # host path.  The fake device draws from the key exactly as the host does.
+    from kmeans_amd import sampling
+    calls = []
+
+    def fake_device(keys, sizes, bases, fraction):
+        assert keys.dtype == np.uint64
+        calls.append(keys.tolist())
+        out = []
+        for key, size, base in zip(keys.tolist(), sizes.tolist(), bases.tolist()):
+            u = sampling._python_random_stream(int(key)).random_sample(size)
+            out.append(np.nonzero(u < fraction)[0] + base)
+        return np.concatenate(out)
+
+    sizes = [40000, 30001, 0, 25000]
+    for num, seed in [(5, -987654321), (17, -(2 ** 63)), (3, -1), (9, 2 ** 64 - 3)]:
+        calls.clear()
+        assert sampling.take_sample(sizes, num, seed, device=fake_device) == sampling.take_sample(sizes, num, seed)
+        assert calls and calls[0] == [abs(seed ^ p) for p in (0, 1, 3)]
+    calls.clear()
+    for seed in (2 ** 64 + 5, -(2 ** 70)):
+        assert sampling.take_sample(sizes, 4, seed, device=fake_device) == sampling.take_sample(sizes, 4, seed)
+    assert not calls or all(max(c) < 2 ** 64 for c in calls)
+
+
 def test_vectorised_sampler_equals_python_sampler():
     from kmeans_amd import sampling
     sizes = [70001, 30000]
@@ -94,7 +121,6 @@ def test_placement_partitions_and_order():
     assert [p.n_local for p in pls] == [400, 600]
     np.testing.assert_array_equal(np.concatenate([p.local_rows for p in pls]), X)
     assert pls[1].row0 == 400
-    np.testing.assert_array_equal(pls[1].host_rows([0, 999, 401]), X[[0, 999, 401]])
     # a bare array is one takeSample partition, cut into row blocks per rank
     pa = [place(X, FakeComm(r, 3)) for r in range(3)]
     assert pa[0].global_sizes == [1000]
@@ -169,6 +195,37 @@ def test_driver_reproduces_reference_with_cpu_engine(golden, cpu_engine, name):
     np.testing.assert_array_equal(labels, g["labels"])
 
 
+def test_predict_reuses_fit_rows_only_for_the_same_object(cpu_engine):
+    # predict reuses the runner (rows resident from fit) only for the very
+    # object fit saw, compared with `is` through a weak reference; a new
+    # dataset, even one allocated where the old one lived, gets its own rows
+    import gc
+    ka = _ka()
+    rng = np.random.default_rng(0)
+    A = rng.standard_normal((600, 4)) + np.repeat(np.eye(4) * 20, 150, axis=0)
+    km = ka.KMeans(k=4, max_iter=5, seed=1)
+    km.verbose = False
+    km.fit(A)
+    fitted = km._runner
+    lab_a = np.asarray(km.predict(A).collect())
+    assert km._runner is fitted
+    B = -A[::-1].copy()
+    lab_b = np.asarray(km.predict(B).collect())
+    want_b = np.argmin(((B[:, None, :] - km.centroids[None]) ** 2).sum(-1), axis=1)
+    np.testing.assert_array_equal(lab_b, want_b)
+    assert not np.array_equal(lab_a, lab_b[::-1]) or np.array_equal(want_b, lab_a[::-1])
+    # a dead referent matches nothing, whatever id() a new object gets
+    from kmeans_amd.kmeans import _deref, _ref_to
+    tmp = np.zeros(3)
+    km._runner_src = _ref_to(tmp)
+    del tmp
+    gc.collect()
+    assert _deref(km._runner_src) is None
+    # a type without weak references (e.g. a list) is held by the model instead
+    L = [1, 2]
+    assert _deref(_ref_to(L)) is L
+
+
 # ------------------------------------------------------ multi-rank over gloo
 def _free_port():
     s = socket.socket()
@@ -218,6 +275,110 @@ def test_two_ranks_gloo_match_single_rank(golden, name):
         np.testing.assert_allclose(sse, g["sse_history"], rtol=1e-9)
         np.testing.assert_array_equal(labels, g["labels"])
     assert res[0][4] and not res[1][4]  # only rank 0 logs, like the single driver
+
+
+class SparkLikeRDD:
+    """Duck-typed PySpark RDD: mapPartitions / mapPartitionsWithIndex run "on
+    the executors" (here: over the partition lists) and collect() returns
+    what reaches the calling rank; it records the partitions whose ROWS came
+    back (count triples are not rows)."""
+
+    def __init__(self, parts, log=None, fn=None):
+        self._parts, self.log, self._fn = parts, (log if log is not None else []), fn
+
+    def getNumPartitions(self):
+        return len(self._parts)
+
+    def cache(self):
+        return self
+
+    def mapPartitions(self, f):
+        return SparkLikeRDD(self._parts, self.log, lambda i, it: f(it))
+
+    def mapPartitionsWithIndex(self, f):
+        return SparkLikeRDD(self._parts, self.log, f)
+
+    def collect(self):
+        out = []
+        for i, p in enumerate(self._parts):
+            got = list(self._fn(i, iter(p)))
+            if any(isinstance(x, np.ndarray) for x in got):
+                self.log.append((i, len(got)))
+            out.extend(got)
+        return out
+
+
+def _shard_rank_main(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import kmeans_amd as ka
+        import cpu_engine as ce
+        from conftest import load_golden
+        ka.KMeans._engine_factory = staticmethod(ce.factory)
+        g = load_golden("test_d")
+        X, P = g["X"], int(g["slices"])
+        n = len(X)
+        parts = [list(X[(i * n) // P:((i + 1) * n) // P]) for i in range(P)]
+        res = {}
+        # a PySpark-like RDD: rows reach this rank only from its partitions
+        rdd = SparkLikeRDD(parts)
+        km = ka.KMeans(k=int(g["k"]), max_iter=int(g["max_iter"]), tolerance=float(g["tol"]), seed=int(g["seed"]),
+                       compute_sse=bool(g["sse"]))
+        km.verbose = False
+        km.fit(rdd)
+        res["spark"] = (km.centroids, km.sse_history, sorted(set(rdd.log)))
+
+        # the package's LocalRDD: only this rank's partitions are materialised
+        touched = []
+
+        class Tracked(ka.LocalRDD):
+            def partition_array(self, i):
+                touched.append(i)
+                return super().partition_array(i)
+
+        lrdd = Tracked([np.asarray(p) for p in parts])
+        km2 = ka.KMeans(k=int(g["k"]), max_iter=int(g["max_iter"]), tolerance=float(g["tol"]), seed=int(g["seed"]),
+                        compute_sse=bool(g["sse"]))
+        km2.verbose = False
+        km2.fit(lrdd)
+        res["local"] = (km2.centroids, km2.sse_history, sorted(set(touched)))
+        q.put((rank, P, [len(p) for p in parts], res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_ingest_only_their_own_partitions(golden):
+    # sharded ingestion (kmeans_spark.py:256 rdd.cache() -> HBM): rank r
+    # materialises only partitions [r P/W, (r+1) P/W); the fit is unchanged
+    import torch.multiprocessing as mp
+    g = golden("test_d")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, P, sizes, r in res:
+        own = list(range((rank * P) // 2, ((rank + 1) * P) // 2))
+        C, sse, log = r["spark"]
+        assert [i for i, _ in log] == [i for i in own if sizes[i]], (rank, log)
+        assert all(cnt == sizes[i] for i, cnt in log)
+        np.testing.assert_allclose(C, g["centroids"], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(sse, g["sse_history"], rtol=1e-9)
+        C2, sse2, touched = r["local"]
+        assert touched == own, (rank, touched)
+        np.testing.assert_allclose(C2, g["centroids"], rtol=1e-9, atol=1e-9)
 
 
 def _sample_rank_main(rank, world, port, q):
