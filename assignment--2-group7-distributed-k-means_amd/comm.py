@@ -7,9 +7,11 @@ partial sums (L169-173) and the ``.sum()`` of partition SSEs (L237).  Here:
 * every rank holds the same centroids and recomputes the same update, so
   there is no broadcast;
 * the only per-iteration exchange is ONE sum all-reduce of the float64
-  ``[k][d+1]`` statistics buffer (the SSE comes out of those statistics in
-  closed form), issued by ``allreduce_stats`` on the device buffer itself
-  (backend ``nccl`` = RCCL over xGMI on MI355X; ``gloo`` on CPU for tests);
+  ``[k][d+1] + 1`` statistics buffer (per-cluster sums and counts, plus the
+  SSE slot: every row's float64 residual to its centroid), issued by
+  ``allreduce_stats`` on the device buffer itself, ordered on the engine's
+  stream (``HipEngine.run_collective``; backend ``nccl`` = RCCL over xGMI on
+  MI355X; ``gloo`` on CPU for tests);
 * a few host-side values (data moments at load time, replacement rows on the
   rare empty-cluster path, the wall-clock seed, predictions) use the small
   helpers below.

@@ -6,7 +6,7 @@ The reference receives a PySpark RDD of ``(d,)`` float arrays built by
 
 * ``LocalRDD`` — this package's stand-in for such an RDD
   (``LocalContext().parallelize(X, numSlices)`` mirrors ``sc.parallelize``),
-* a real PySpark RDD (anything with ``glom().collect()``),
+* a real PySpark RDD (anything with ``mapPartitions`` / ``mapPartitionsWithIndex``),
 * a NumPy array ``[n][d]`` (one partition),
 * ``DeviceBlobs`` — a synthetic Gaussian-blob dataset generated directly in
   HBM (benchmarks; nothing on the host).

@@ -120,10 +120,23 @@ class HipEngine:
         self._c(self.lib.km_assign_stats(self.ctx), "km_assign_stats")
 
     def run_collective(self, fn) -> None:
-        """Run ``fn(stats_tensor)`` (an in-place all-reduce) ordered on this
-        context's stream."""
+        """Run ``fn(stats_tensor, async_op=True)`` (an in-place all-reduce)
+        ordered on this context's HIP stream, with no host synchronisation.
+
+        Ordering (torch ProcessGroupNCCL = RCCL here): the collective runs on
+        the process group's own stream, which first waits on the CURRENT
+        stream -- made ``self._tstream``, the wrapper of the engine's stream,
+        so the all-reduce reads the statistics only after km_assign_stats
+        wrote them; ``work.wait()`` then "lets the current stream wait for the
+        NCCL to finish" (torch/include/torch/csrc/distributed/c10d/
+        ProcessGroupNCCL.hpp:289-317 and WorkNCCL::wait/synchronize,
+        :355-371: a stream-level wait, not a host block), so km_update /
+        km_update_async enqueued next on the engine stream read the summed
+        buffer.  gloo (CPU tensors) completes inside wait()."""
         with self._torch.cuda.stream(self._tstream):
-            fn(self._stats_t)
+            work = fn(self._stats_t, async_op=True)
+            if work is not None:
+                work.wait()
 
     def update(self) -> Tuple[_lib.KmStatus, np.ndarray]:
         st = _lib.KmStatus()

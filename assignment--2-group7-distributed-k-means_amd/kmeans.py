@@ -230,7 +230,18 @@ class KMeans:
     """Distributed K-Means, MI355X-native (kmeans_spark.py:19-47).
 
     Parameters: k, max_iter, tolerance (max centroid shift), seed (sampling of
-    the initial centroids), compute_sse (track the SSE each iteration)."""
+    the initial centroids), compute_sse (track the SSE each iteration).
+
+    Compute contract: rows are stored in HBM as float32, rounded once at load
+    (a float64 input is not copied at full precision); every row the fit uses
+    afterwards -- assignment, per-cluster sums, the takeSample initial and
+    replacement centroids -- is that rounded row, and all arithmetic on it
+    (distances to decide labels, sums, centroids, SSE) is float64 with the
+    reference's NumPy rounding where it decides a label.  The result is
+    therefore the reference's result on ``X.astype(float32)``: identical for
+    float32-representable data, within float32 rounding (~1e-7 relative of the
+    data scale) of the reference on raw float64 rows.  Centroids are returned
+    in the input's float dtype."""
 
     _engine_factory = None  # test seam: tests/ inject a CPU engine for host-logic tests
 

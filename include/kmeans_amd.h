@@ -69,8 +69,9 @@ typedef struct km_status {
 typedef struct km_info {
   int64_t n;         /* local rows                                    */
   int32_t d, dp;     /* features, padded row stride                   */
-  int32_t k, kp;     /* clusters, padded to a multiple of 32          */
-  int32_t path;      /* 1 = small direct-form path, 2 = MFMA bf16x3   */
+  int32_t k, kp;     /* clusters, padded to a multiple of 64          */
+  int32_t path;      /* 1 = small direct-form path, 2 = MFMA fp16x3 screen
+                        (k_fused / k_assign_mfma; k_assign_wide for dp > 256) */
   int32_t n_cu;      /* compute units of the device                   */
   int32_t device;
   int32_t fused_stats;

@@ -154,6 +154,39 @@ def test_one_step_vs_oracle(n, d, k, centers):
     assert _check_labels(X, ref["centroids"], labels) == 0
 
 
+@pytest.mark.parametrize("n,d,k,slices", [(30000, 16, 12, 4), (20000, 100, 40, 3)])
+def test_raw_float64_input_is_the_reference_on_its_fp32_rounding(n, d, k, slices):
+    # raw float64 make_blobs-style rows (not fp32-representable).  The compute
+    # contract (KMeans docstring): rows are rounded to float32
+    # once at load and every row the fit uses -- assignment, sums, the
+    # takeSample initial centroids -- is the rounded row.  So the result IS the
+    # reference's on X.astype(float32) (bit-exact labels, 1e-9 centroids/SSE),
+    # and within float32 rounding of the reference's on the raw rows.
+    ka = _km()
+    rng = np.random.default_rng(n + d)
+    centers = rng.uniform(-10, 10, (k, d))
+    X = centers[rng.integers(0, k, n)] + rng.standard_normal((n, d))
+    assert not np.array_equal(X, X.astype(np.float32).astype(np.float64))
+    km = ka.KMeans(k=k, max_iter=8, tolerance=1e-4, seed=11, compute_sse=True)
+    km.verbose = False
+    rdd = ka.LocalContext().parallelize(X, slices)
+    km.fit(rdd)
+    labels = np.asarray(km.predict(rdd).collect())
+    X32 = X.astype(np.float32).astype(np.float64)
+    ref32 = orc.lloyd_fit(X32, k, 8, 1e-4, 11, True, slices)
+    np.testing.assert_allclose(km.centroids, ref32["centroids"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(km.sse_history, ref32["sse_history"], rtol=1e-9)
+    np.testing.assert_array_equal(labels, orc.assign(X32, ref32["centroids"])[0])
+    # against the raw-float64 reference: same run, float32-rounding close
+    ref64 = orc.lloyd_fit(X, k, 8, 1e-4, 11, True, slices)
+    assert len(ref64["sse_history"]) == len(km.sse_history)
+    np.testing.assert_allclose(km.centroids, ref64["centroids"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(km.sse_history, ref64["sse_history"], rtol=1e-6)
+    lab64, _, gap = orc.assign(X, ref64["centroids"])
+    bad = np.nonzero(labels != lab64)[0]
+    assert np.all(gap[bad] < BAND), f"{len(bad)} label mismatches outside the 1e-6 band"
+
+
 def test_randn_many_iterations_vs_oracle():
     # random noise (test_b style): many near-ties, stresses the exact resolve
     rng = np.random.RandomState(42)
