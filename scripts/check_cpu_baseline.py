@@ -7,8 +7,12 @@ kmeans_spark.py:169-171).  This script times, on one core and on the same
 (X, C), that restatement against the reference's own closures: the reference
 module imported unmodified with the in-memory PySpark stand-in
 (tests/golden/_pyspark_stub, as tests/golden/make_golden.py does), running
-``KMeans._assign_to_clusters`` + ``KMeans._update_centroids`` over one
-partition.  The two sides run as adjacent pairs (reference, then oracle, on
+its per-point work over one partition: ``KMeans._assign_to_clusters`` and
+the ``reduceByKey`` with the reference's own combine lambda (captured from
+``KMeans._update_centroids`` through a recording proxy, kmeans_spark.py:169-171).
+The driver-side rest of ``_update_centroids`` (a Python loop over the k
+clusters per iteration) is not per-point work and is left out, as the
+oracle's extrapolation to N leaves it out.  The two sides run as adjacent pairs (reference, then oracle, on
 the same sample), repeated; the verdict is the MEDIAN of the per-pair
 throughput ratios, which cancels the slow drift of a shared VM's speed (+-15 %
 between runs here) and ignores outliers.  Both are pinned to one core, timed
@@ -43,9 +47,34 @@ SHAPES = [  # (name, d, k, points per repetition, repetitions): the BASELINE.jso
 ]
 
 
+class _Captured(Exception):
+    pass
+
+
+class _RecordingRDD:
+    """Stands in for the assigned RDD to learn the function
+    ``_update_centroids`` passes to ``reduceByKey`` (L169-171)."""
+
+    def reduceByKey(self, f):
+        self.f = f
+        raise _Captured
+
+
+def reference_combine(ref, sc, C):
+    km = ref.KMeans(k=len(C), max_iter=1, tolerance=1e-4, seed=42, compute_sse=False)
+    km.centroids = C.copy()
+    rec = _RecordingRDD()
+    try:
+        km._update_centroids(rec, None, sc, sc.broadcast(C))
+    except _Captured:
+        return rec.f
+    raise RuntimeError("reduceByKey was not reached")
+
+
 def time_reference(ref, X, C, reps):
     sc = ref.SparkContext(appName="cpu-baseline-check")
     rdd = sc.parallelize(X, 1)
+    combine = reference_combine(ref, sc, C)
     best = float("inf")
     for _ in range(reps):
         km = ref.KMeans(k=len(C), max_iter=1, tolerance=1e-4, seed=42, compute_sse=False)
@@ -53,7 +82,7 @@ def time_reference(ref, X, C, reps):
         bc = sc.broadcast(C)
         t0 = time.process_time()
         assigned = km._assign_to_clusters(rdd, bc)             # L147-161 (eager in the stand-in)
-        km._update_centroids(assigned, rdd, sc, bc)            # L169-206
+        assigned.reduceByKey(combine)                          # L169-171, the reference's lambda
         best = min(best, time.process_time() - t0)
     return len(X) / best
 

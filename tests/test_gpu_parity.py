@@ -167,18 +167,22 @@ def test_raw_float64_input_is_the_reference_on_its_fp32_rounding(n, d, k, slices
     centers = rng.uniform(-10, 10, (k, d))
     X = centers[rng.integers(0, k, n)] + rng.standard_normal((n, d))
     assert not np.array_equal(X, X.astype(np.float32).astype(np.float64))
-    km = ka.KMeans(k=k, max_iter=8, tolerance=1e-4, seed=11, compute_sse=True)
+    class Seeded(ka.KMeans):
+        def _empty_seed(self):          # int(time.time()) at L196, pinned for the comparison
+            return 1234
+
+    km = Seeded(k=k, max_iter=8, tolerance=1e-4, seed=11, compute_sse=True)
     km.verbose = False
     rdd = ka.LocalContext().parallelize(X, slices)
     km.fit(rdd)
     labels = np.asarray(km.predict(rdd).collect())
     X32 = X.astype(np.float32).astype(np.float64)
-    ref32 = orc.lloyd_fit(X32, k, 8, 1e-4, 11, True, slices)
+    ref32 = orc.lloyd_fit(X32, k, 8, 1e-4, 11, True, slices, empty_seed=lambda: 1234)
     np.testing.assert_allclose(km.centroids, ref32["centroids"], rtol=1e-9, atol=1e-9)
     np.testing.assert_allclose(km.sse_history, ref32["sse_history"], rtol=1e-9)
     np.testing.assert_array_equal(labels, orc.assign(X32, ref32["centroids"])[0])
     # against the raw-float64 reference: same run, float32-rounding close
-    ref64 = orc.lloyd_fit(X, k, 8, 1e-4, 11, True, slices)
+    ref64 = orc.lloyd_fit(X, k, 8, 1e-4, 11, True, slices, empty_seed=lambda: 1234)
     assert len(ref64["sse_history"]) == len(km.sse_history)
     np.testing.assert_allclose(km.centroids, ref64["centroids"], rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(km.sse_history, ref64["sse_history"], rtol=1e-6)

@@ -50,6 +50,27 @@ def test_product_library_has_no_diagnostic_kernels():
                                           text=True, check=True).stdout
 
 
+def test_exact_helpers_forbid_contraction():
+    # hipcc fuses `acc + t * t` into v_fma_f64 unless `#pragma clang fp
+    # contract(off)` covers the add; a fused square is not NumPy's rounding
+    # (kmeans_spark.py:153).  Every helper of km_exact.h that adds or
+    # multiplies doubles opens with the pragma (the round-1 scan variant whose
+    # own multi-point helper lacked it computed wrong norms; DESIGN.md section
+    # 2).  Comparison-only helpers and sqrt wrappers over pragma'd sums are
+    # listed explicitly.
+    src = open(os.path.join(ROOT, "assignment--2-group7-distributed-k-means_amd", "csrc", "km_exact.h")).read()
+    no_arith = {"np_better", "np_pick_second", "np_norm_d", "np_norm"}
+    heads = list(re.finditer(r"__device__[^;{]*?\b(np_\w+)\s*\(", src))
+    assert len(heads) >= 12, [m.group(1) for m in heads]
+    for m in heads:
+        name = m.group(1)
+        body = src[src.index("{", m.end()) + 1:][:200]
+        if name in no_arith:
+            assert "+" not in body.split("}")[0].replace("++", "") or name.startswith("np_norm"), name
+            continue
+        assert body.lstrip().startswith("#pragma clang fp contract(off)"), f"{name}: no contract(off) pragma"
+
+
 def test_no_cpu_fallback_without_gpu():
     import torch
     if torch.cuda.is_available():
