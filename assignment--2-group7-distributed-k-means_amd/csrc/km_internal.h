@@ -124,9 +124,13 @@ hipError_t launch_sse(const float* X, const Geometry& g, const int32_t* labels, 
 // set); stop_tol >= 0 lets k_finalize raise it (KM_STOP_*), < 0 never
 // dev_repair: empty clusters are repaired on the device (launch_repair), so
 // they neither raise the gate nor allow a convergence stop here
-hipError_t launch_update(const double* stats, const double* C64_old, const Geometry& g, double* C64_new,
+// clear / C32, cmax (one-workgroup update only, update_one_ok): zero the
+// statistics after use and write the small path's images of the new centroids
+bool update_one_ok(const Geometry& g);
+hipError_t launch_update(double* stats, const double* C64_old, const Geometry& g, double* C64_new,
                          double* work, int64_t* counts, const uint32_t* qcount, uint32_t nq, DevStatus* status,
-                         int* gate, double stop_tol, int dev_repair, hipStream_t s);
+                         int* gate, double stop_tol, int dev_repair, hipStream_t s, int clear = 0,
+                         float* C32 = nullptr, float* cmax = nullptr);
 hipError_t launch_sum_x(const float* X, const Geometry& g, double* out, hipStream_t s);
 hipError_t launch_scatter_rows(const int64_t* ids, const double* rows, int32_t n, int d, double* C, hipStream_t s);
 hipError_t launch_gather_rows(const float* X, const Geometry& g, const int64_t* idx, int32_t n, double* out,

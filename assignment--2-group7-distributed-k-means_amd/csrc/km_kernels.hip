@@ -2813,13 +2813,19 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ wor
 // k_update + k_finalize in one workgroup for small k (c1 / c2 shapes, where
 // the two launches are mostly launch gaps): same arithmetic and
 // reduction order per cluster (lanes over features, wave sums), then the
-// status record and the batch gate as k_finalize.
-__global__ __launch_bounds__(1024) void k_update_one(const double* __restrict__ stats, const double* __restrict__ old,
+// status record and the batch gate as k_finalize.  In a batch it also ends
+// the iteration's other small launches: `clear` zeroes the statistics it
+// consumed (the next assign accumulates into them; no memset launch), and
+// with C32 it writes the small path's images of the new centroids -- the
+// fp32 copy and max ||c||, exactly as k_prep_small (same per-lane fma order
+// over f < dp, same wave sums) -- so the next assign needs no prep launch.
+__global__ __launch_bounds__(1024) void k_update_one(double* __restrict__ stats, const double* __restrict__ old,
                                                      int k, int d, double* __restrict__ out,
                                                      int64_t* __restrict__ counts, const double* __restrict__ sse,
                                                      const uint32_t* __restrict__ qcount, uint32_t nq,
                                                      DevStatus* __restrict__ st, int* __restrict__ gate,
-                                                     double stop_tol, int dev_repair) {
+                                                     double stop_tol, int dev_repair, int clear, float* __restrict__ C32,
+                                                     float* __restrict__ cmax, int dp, int kp) {
   if (*gate) {
     if (threadIdx.x == 0) {
       st->ran = 0;
@@ -2829,31 +2835,46 @@ __global__ __launch_bounds__(1024) void k_update_one(const double* __restrict__ 
   }
   __shared__ double s_max[16];
   __shared__ int s_emp[16], s_nf[16], s_q[16], s_qf[16];
+  __shared__ unsigned int s_cm[16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int d1 = d + 1;
   double mx = 0.0;
   int emp = 0, nf = 0, qa = 0, qb = 0;
+  unsigned int cmb = 0u;  // max ||c|| bits (k_prep_small)
   for (int j = wave; j < k; j += nw) {
     const double cnt = stats[(size_t)j * d1 + d];
-    double sh = 0.0, nfl = 0.0;
-    for (int f = lane; f < d; f += 64) {
-      const double S = stats[(size_t)j * d1 + f];
-      const double o = old[(size_t)j * d + f];
-      const double nv = (cnt > 0.0) ? S / cnt : o;
-      out[(size_t)j * d + f] = nv;
-      const double df = nv - o;
-      sh = fma(df, df, sh);
-      if (!isfinite(nv)) nfl = 1.0;
+    double sh = 0.0, nfl = 0.0, nn = 0.0;
+    for (int f = lane; f < (C32 ? dp : d); f += 64) {
+      if (f < d) {
+        const double S = stats[(size_t)j * d1 + f];
+        const double o = old[(size_t)j * d + f];
+        const double nv = (cnt > 0.0) ? S / cnt : o;
+        out[(size_t)j * d + f] = nv;
+        const double df = nv - o;
+        sh = fma(df, df, sh);
+        if (!isfinite(nv)) nfl = 1.0;
+        if (C32) {
+          nn = fma(nv, nv, nn);
+          C32[(size_t)j * dp + f] = (float)nv;
+        }
+      } else {
+        nn = fma(0.0, 0.0, nn);
+        C32[(size_t)j * dp + f] = 0.0f;
+      }
     }
     sh = wave_sum(sh);
     nfl = wave_sum(nfl);
+    if (C32) nn = wave_sum(nn);
     if (lane == 0) {
       counts[j] = (int64_t)cnt;
       mx = fmax(mx, sh);
       nf |= (nfl != 0.0);
       emp += (cnt == 0.0);
+      if (C32) cmb = max(cmb, __float_as_uint(sqrtf((float)nn) * 1.0001f + 1e-30f));
     }
   }
+  if (C32)  // padded rows k <= j < kp stay zero (as k_prep_small writes them)
+    for (int i = threadIdx.x; i < (kp - k) * dp; i += blockDim.x) C32[(size_t)k * dp + i] = 0.0f;
   for (uint32_t w = threadIdx.x; w < nq; w += blockDim.x) {
     qa += (int)qcount[2 * w];
     qb += (int)qcount[2 * w + 1];
@@ -2868,8 +2889,13 @@ __global__ __launch_bounds__(1024) void k_update_one(const double* __restrict__ 
     s_nf[wave] = nf;
     s_q[wave] = qa;
     s_qf[wave] = qb;
+    s_cm[wave] = cmb;
   }
   __syncthreads();
+  const double sse_v = *sse;
+  __syncthreads();  // every read of the statistics is done
+  if (clear)
+    for (int i = threadIdx.x; i < k * d1 + 1; i += blockDim.x) stats[i] = 0.0;
   if (threadIdx.x == 0) {
     for (int w = 1; w < nw; ++w) {
       mx = fmax(mx, s_max[w]);
@@ -2877,10 +2903,12 @@ __global__ __launch_bounds__(1024) void k_update_one(const double* __restrict__ 
       nf |= s_nf[w];
       qa += s_q[w];
       qb += s_qf[w];
+      cmb = max(cmb, s_cm[w]);
     }
+    if (C32) *cmax = __uint_as_float(cmb);
     const double ms = sqrt(mx);
     st->max_shift = ms;
-    st->sse = *sse;
+    st->sse = sse_v;
     st->n_empty = emp;
     st->nonfinite = nf;
     st->q_full = qb;
@@ -2901,14 +2929,19 @@ __global__ __launch_bounds__(1024) void k_update_one(const double* __restrict__ 
   }
 }
 
-hipError_t launch_update(const double* stats, const double* C64_old, const Geometry& g, double* C64_new,
+bool update_one_ok(const Geometry& g) { return g.k <= 64 && (size_t)g.k * g.d <= 16384; }
+
+hipError_t launch_update(double* stats, const double* C64_old, const Geometry& g, double* C64_new,
                          double* work, int64_t* counts, const uint32_t* qcount, uint32_t nq, DevStatus* status,
-                         int* gate, double stop_tol, int dev_repair, hipStream_t s) {
-  if (g.k <= 64 && (size_t)g.k * g.d <= 16384) {  // at most 4 clusters per wave (c3: 2 launches, 11 vs 37 us)
+                         int* gate, double stop_tol, int dev_repair, hipStream_t s, int clear, float* C32,
+                         float* cmax) {
+  if (update_one_ok(g)) {  // at most 4 clusters per wave (c3: 2 launches, 11 vs 37 us)
     hipLaunchKernelGGL(k_update_one, dim3(1), dim3(1024), 0, s, stats, C64_old, g.k, g.d, C64_new, counts,
-                       stats + (size_t)g.k * (g.d + 1), qcount, nq, status, gate, stop_tol, dev_repair);
+                       stats + (size_t)g.k * (g.d + 1), qcount, nq, status, gate, stop_tol, dev_repair, clear, C32,
+                       cmax, g.dp, g.kp);
     return hipGetLastError();
   }
+  if (clear || C32) return hipErrorInvalidValue;  // only the one-workgroup update clears / prepares
   hipLaunchKernelGGL(k_update, dim3(g.k), dim3(64), 0, s, stats, C64_old, g.k, g.d, C64_new, work, counts, gate);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

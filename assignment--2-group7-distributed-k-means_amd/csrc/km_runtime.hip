@@ -78,6 +78,13 @@ struct km_ctx {
   // exact resolution (the refinement costs ~4% where the global test settles
   // nearly every row, and saves most of the exact work where it does not)
   bool refine = true;
+  // statistics already zero (the batch update cleared them): no memset
+  bool stats_clean = false;
+  // device repair kernels enqueued in batches: armed for the first batch
+  // after new centroids (where empties occur) and after an empty stop;
+  // disarmed by a batch without empties (then an empty stops the batch and
+  // the host repairs it with the same policy)
+  bool rep_armed = false;
   // data
   float* X = nullptr;
   int32_t* labels = nullptr;
@@ -307,7 +314,8 @@ int run_assign(km_ctx* c, bool with_stats) {
   c->ql = km::QLayout{0, 0};
   const bool sse = with_stats && c->want_sse;
   double* sse_slot = c->stats + (size_t)g.k * (g.d + 1);
-  if (with_stats) KM_HIP(hipMemsetAsync(c->stats, 0, sizeof(double) * stats_len(g), c->stream));
+  if (with_stats && !c->stats_clean) KM_HIP(hipMemsetAsync(c->stats, 0, sizeof(double) * stats_len(g), c->stream));
+  if (with_stats) c->stats_clean = false;
   if (c->path == 1) {
     ProfScope ps(c, KM_K_ASSIGN);
     KM_HIP(km::launch_assign_small(c->X, g, c->C32, c->C64_cur, c->cmax, c->labels, c->stats, with_stats ? 1 : 0,
@@ -590,6 +598,7 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
     KM_HIP(hipMalloc(&c->hist_counts, sizeof(int64_t) * (size_t)k * KM_MAX_BATCH));
     KM_HIP(hipHostMalloc(&c->hist_counts_host, sizeof(int64_t) * (size_t)k * KM_MAX_BATCH, hipHostMallocDefault));
     c->stats = c->stats_own;
+    c->stats_clean = false;
     c->k_alloc = k;
     if (km::small_path_ok(c->g))
       c->path = 1;
@@ -605,6 +614,7 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
   KM_HIP(hipStreamSynchronize(c->stream));
   c->have_c = true;
   c->refine = true;
+  c->rep_armed = c->rep_enabled;
   return KM_OK;
 }
 
@@ -635,6 +645,7 @@ int km_stats_buffer(km_ctx* c, void** p, int64_t* len) {
 int km_bind_stats_buffer(km_ctx* c, void* p) {
   KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_bind_stats_buffer: set centroids first");
   c->stats = p ? reinterpret_cast<double*>(p) : c->stats_own;
+  c->stats_clean = false;
   return KM_OK;
 }
 
@@ -707,6 +718,7 @@ int km_set_layout(km_ctx* c, const int64_t* sizes, int32_t nparts, int64_t row0,
     KM_HIP(hipMemcpy(c->rep_bases, bases.data(), sizeof(int64_t) * nparts, hipMemcpyHostToDevice));
     c->rep_enabled = true;
   }
+  c->rep_armed = c->rep_enabled;
   return KM_OK;
 }
 
@@ -726,13 +738,20 @@ int km_update_async(km_ctx* c, double tol, int64_t empty_seed) {
   KM_REQUIRE(tol >= 0.0, KM_ERR_ARG, "km_update_async: tolerance must be >= 0");
   KM_HIP(hipSetDevice(c->device));
   const int slot = c->batch_n;
+  const bool repair = c->rep_enabled && c->rep_armed;
+  // one-workgroup update: clears the statistics and, on the small path with
+  // no repair behind it, writes the next assign's centroid images itself
+  const bool one = km::update_one_ok(c->g);
+  const bool fold_prep = one && c->path == 1 && !repair;
   {
     ProfScope ps(c, KM_K_UPDATE);
     KM_HIP(km::launch_update(c->stats, c->C64_cur, c->g, c->C64_new, c->work,
                              c->hist_counts + (size_t)slot * c->g.k, c->qcount, c->ql.nwaves, c->hist + slot,
-                             c->gate, tol, c->rep_enabled ? 1 : 0, c->stream));
+                             c->gate, tol, repair ? 1 : 0, c->stream, one ? 1 : 0, fold_prep ? c->C32 : nullptr,
+                             fold_prep ? c->cmax : nullptr));
   }
-  if (c->rep_enabled) {
+  if (one) c->stats_clean = true;
+  if (repair) {
     KM_REQUIRE(empty_seed >= 0, KM_ERR_ARG, "km_update_async: negative empty-cluster seed");
     const int rc = ensure_repair(c);
     if (rc != KM_OK) return rc;
@@ -746,7 +765,9 @@ int km_update_async(km_ctx* c, double tol, int64_t empty_seed) {
   // speculative commit (kmeans_spark.py:307): the next iteration reads the
   // new centroids; a stopped batch's later kernels (prep included) no-op and
   // km_batch_end restores the state after the last iteration that ran
-  {
+  if (fold_prep) {
+    c->prep_of = c->C64_new;  // written by the update (it ran whenever the next assign runs)
+  } else {
     const int rc = prep(c, c->C64_new);
     if (rc != KM_OK) return rc;
   }
@@ -780,6 +801,12 @@ int km_batch_end(km_ctx* c, km_status* st, int64_t* counts, int32_t* n_ran) {
     // the iteration that raised the gate had its own prep gated too
     c->prep_of = c->hist_host[ran - 1].stop ? nullptr : c->C64_new;
     note_queue(c, c->hist_host[ran - 1]);
+    if (c->rep_enabled) {
+      bool any_empty = false;
+      for (int i = 0; i < ran; ++i) any_empty |= c->hist_host[i].n_empty > 0;
+      // an empty stop (disarmed) re-arms; a batch without empties disarms
+      c->rep_armed = any_empty;
+    }
   } else if (m > 0) {
     c->C64_cur = c->slot_cur[0];
     c->C64_new = c->slot_new[0];
@@ -810,6 +837,7 @@ int km_replace_rows(km_ctx* c, const int32_t* ids, const double* rows, int32_t n
   if (n == 0) return KM_OK;
   if (c->prep_of == c->C64_new) c->prep_of = nullptr;  // its images are stale now
   c->refine = true;
+  c->rep_armed = c->rep_enabled;
   std::vector<int64_t> ids64(n);
   for (int i = 0; i < n; ++i) {
     KM_REQUIRE(ids[i] >= 0 && ids[i] < c->g.k, KM_ERR_ARG, "km_replace_rows: cluster id out of range");
