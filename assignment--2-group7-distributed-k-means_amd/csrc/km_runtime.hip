@@ -148,8 +148,9 @@ struct km_ctx {
   int64_t* rep_picks = nullptr;   // [nparts][cp]
   int64_t* rep_samples = nullptr; // [nparts * cp]
   // staging
-  float* pinned = nullptr;
+  float* pinned = nullptr;      // two staging halves of pinned_floats each
   size_t pinned_floats = 0;
+  hipEvent_t staged[2] = {nullptr, nullptr};  // a half's copy has left it
   // profiling
   int prof = 0;                  // bitmask of KM_K_* phases timed with events
   const double* prep_of = nullptr;  // the centroid buffer the derived images were built from
@@ -428,6 +429,8 @@ int km_destroy(km_ctx* c) {
   free_centroids(c);
   free_data(c);
   hfree(c->pinned);
+  for (auto& e : c->staged)
+    if (e) (void)hipEventDestroy(e);
   for (auto& v : c->ev)
     for (auto& p : v) {
       (void)hipEventDestroy(p.first);
@@ -509,23 +512,33 @@ int km_load_rows(km_ctx* c, int64_t row0, const float* rows, int64_t nrows) {
   KM_REQUIRE(rows, KM_ERR_ARG, "km_load_rows: null rows");
   KM_HIP(hipSetDevice(c->device));
   const int d = c->g.d, dp = c->g.dp;
-  const size_t chunk_floats = (size_t)16 << 20;  // 64 MiB pinned staging
+  // double-buffered pinned staging: the host fills one half while the DMA
+  // of the other is in flight (one event per half, one sync at the end)
+  const size_t chunk_floats = (size_t)16 << 20;  // 2 x 64 MiB
   if (!c->pinned) {
-    KM_HIP(hipHostMalloc(&c->pinned, chunk_floats * sizeof(float), hipHostMallocDefault));
+    KM_HIP(hipHostMalloc(&c->pinned, 2 * chunk_floats * sizeof(float), hipHostMallocDefault));
     c->pinned_floats = chunk_floats;
+    for (auto& e : c->staged) KM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   const int64_t per = std::max<int64_t>(1, (int64_t)(c->pinned_floats / d));
-  for (int64_t r = 0; r < nrows; r += per) {
+  KM_REQUIRE((size_t)d <= c->pinned_floats, KM_ERR_ARG, "km_load_rows: row wider than the staging buffer");
+  int half = 0;
+  bool used[2] = {false, false};
+  for (int64_t r = 0; r < nrows; r += per, half ^= 1) {
     const int64_t m = std::min(per, nrows - r);
-    memcpy(c->pinned, rows + r * d, sizeof(float) * m * d);
-    KM_HIP(hipMemcpy2DAsync(c->X + (row0 + r) * dp, sizeof(float) * dp, c->pinned, sizeof(float) * d,
+    float* buf = c->pinned + (size_t)half * c->pinned_floats;
+    if (used[half]) KM_HIP(hipEventSynchronize(c->staged[half]));  // its previous copy is done
+    memcpy(buf, rows + r * d, sizeof(float) * m * d);
+    KM_HIP(hipMemcpy2DAsync(c->X + (row0 + r) * dp, sizeof(float) * dp, buf, sizeof(float) * d,
                             sizeof(float) * d, m, hipMemcpyHostToDevice, c->stream));
+    KM_HIP(hipEventRecord(c->staged[half], c->stream));
+    used[half] = true;
     KM_HIP(km::launch_absmax(c->X + (row0 + r) * dp, m * dp, c->xabs, c->stream));
     km::Geometry sub = c->g;
     sub.n = m;
     KM_HIP(km::launch_row_norm(c->X + (row0 + r) * dp, sub, c->xnorm + row0 + r, c->stream));
-    KM_HIP(hipStreamSynchronize(c->stream));
   }
+  KM_HIP(hipStreamSynchronize(c->stream));
   return KM_OK;
 }
 

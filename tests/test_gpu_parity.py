@@ -191,6 +191,25 @@ def test_raw_float64_input_is_the_reference_on_its_fp32_rounding(n, d, k, slices
     assert np.all(gap[bad] < BAND), f"{len(bad)} label mismatches outside the 1e-6 band"
 
 
+def test_load_rows_multi_chunk_staging():
+    # km_load_rows streams through two 64 MiB pinned halves (262,144 rows of
+    # d = 64 each): rows at and around the chunk boundaries come back exactly,
+    # column sums match (float32 rows, float64 sums)
+    from kmeans_amd.engine import HipEngine
+    rng = np.random.default_rng(9)
+    n, d = 700_001, 64
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    eng = HipEngine(0)
+    try:
+        eng.load_host(X)
+        per = (16 << 20) // d
+        idx = np.array([0, per - 1, per, per + 1, 2 * per - 1, 2 * per, n - 1], dtype=np.int64)
+        np.testing.assert_array_equal(eng.gather_rows(idx), X[idx].astype(np.float64))
+        np.testing.assert_allclose(eng.sum_x(), X.astype(np.float64).sum(axis=0), rtol=1e-9, atol=1e-6)
+    finally:
+        eng.close()
+
+
 def test_randn_many_iterations_vs_oracle():
     # random noise (test_b style): many near-ties, stresses the exact resolve
     rng = np.random.RandomState(42)

@@ -4,6 +4,7 @@ test-only oracle engine) against the reference's golden vectors, and the
 multi-rank path over gloo (world size 2)."""
 import contextlib
 import io
+import json
 import os
 import re
 import socket
@@ -245,6 +246,32 @@ def test_predict_reuses_fit_rows_only_for_the_same_object(cpu_engine):
     # a type without weak references (e.g. a list) is held by the model instead
     L = [1, 2]
     assert _deref(_ref_to(L)) is L
+
+
+def test_speedup_table_from_bench_lines(tmp_path):
+    # test_e counterpart (kmeans_spark.py:543-621): bench lines of 1/2/4/8
+    # GPUs -> the reference's timing table and the ideal-vs-actual figure
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("speedup", os.path.join(ROOT, "scripts", "speedup.py"))
+    sp = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sp)
+    lines = [{"metric": "m", "value": v, "unit": "Lloyd it/s", "n_gpus": n, "ms_per_step": 1e3 / v}
+             for n, v in [(1, 88.0), (2, 170.0), (4, 330.0), (8, 600.0)]]
+    f1 = tmp_path / "n1_2.json"
+    f1.write_text("\n".join(json.dumps(o) for o in lines[:2]))
+    f2 = tmp_path / "scale.json"   # a driver-style wrapper holding the rest
+    f2.write_text(json.dumps({"runs": [{"n": 4, "parsed": lines[2]}, {"n": 8, "tail": json.dumps(lines[3]) + "\n"}]}))
+    rows = sp.speedup_table(sp.load_runs([str(f1), str(f2)]))
+    assert [r[0] for r in rows] == [1, 2, 4, 8]
+    np.testing.assert_allclose([r[2] for r in rows], [1.0, 170 / 88, 330 / 88, 600 / 88])
+    np.testing.assert_allclose([r[3] for r in rows], [1.0, 170 / 176, 330 / 352, 600 / 704])
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        sp.print_table(rows)
+        png = sp.plot(rows, str(tmp_path / "speedup_graph.png"), "Number of GPUs")
+    assert "GPUs:  8 | Time:   0.0017s | Speedup: 6.8182x" in buf.getvalue()
+    if png:
+        assert os.path.getsize(png) > 1000
 
 
 # ------------------------------------------------------ multi-rank over gloo
