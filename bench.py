@@ -39,6 +39,8 @@ CONFIGS = {
     # c5 with poor seeds (BASELINE.json configs[4]): 3 data rows + 4093 far
     # points, so the first step replaces 4093 empty clusters (on the device)
     "c5_poor": (50_000_000, 128, 4096, 4096),
+    # rows wider than 256 features (k_assign_wide; not a BASELINE config)
+    "w784": (4_000_000, 784, 256, 256),
 }
 POOR_SEEDS = {"c5_poor"}
 HBM_PEAK_GBS = 8000.0                 # MI355X spec (MI355X_MICROARCH.md)
@@ -200,7 +202,9 @@ def main():
             traffic = None
     if info["path"] == 2 and dom == "assign":
         ach = flops_launch / avg_s / 1e12
-        kname = "k_fused (fp16x3 screen + f64 sums)" if info["fused_stats"] else "k_assign_mfma (fp16x3 screen)"
+        kname = ("k_fused (fp16x3 screen + f64 sums)" if info["fused_stats"] else
+                 "k_assign_wide (fp16x3 screen, feature chunks)" if info["dp"] > 256 else
+                 "k_assign_mfma (fp16x3 screen)")
         roof = {"bound": "mfma", "achieved": ach, "peak": F16X3_EFFECTIVE_TFLOPS, "unit": "TFLOP/s",
                 "frac": ach / F16X3_EFFECTIVE_TFLOPS, "traffic": traffic, "kernel": kname,
                 "peak_note": "dense f16 MFMA 2516.6 TF / 3 (fp16x3 split: 3 MFMAs per product); "
