@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(HERE, "libkmeans_amd.so")
 ROOT = os.path.dirname(HERE)
 HEADER = os.path.join(ROOT, "include", "kmeans_amd.h")
 
-KM_ABI_VERSION = 2
+KM_ABI_VERSION = 3
 KM_OK = 0
 KM_EMPTY = 1
 
@@ -66,6 +66,8 @@ SIGNATURES = {
     "km_generate_blobs": [_P, _I64, _I32, _I64, _I32, ctypes.c_float, ctypes.c_float, ctypes.c_uint64],
     "km_sum_x": [_P, _PD],
     "km_set_sse": [_P, _I32],
+    "km_set_screen": [_P, _I32],
+    "km_get_screen": [_P, ctypes.POINTER(ctypes.c_int32)],
     "km_set_centroids": [_P, _PD, _I32, _I32],
     "km_get_centroids": [_P, _I32, _PD],
     "km_assign_stats": [_P],

@@ -98,11 +98,19 @@ void dump_fused_stamps();  // diagnostic build only (KM_ABLATE=7)
 // per-key refinement in k_fused, on the last queue fraction: a cost choice
 // with no effect on results, which are exact either way).
 int diag_env(const char* name, int dflt);
+// Screen of the fused kernel: fp16x3 with the global bound (X3), plus the
+// per-key refinement (X3_REFINE), or the fast screen k_fused1 (one fp16 image,
+// pairwise bound) with the row as one fp16 part (FAST1) or hi + lo (FAST2).
+// Results are exact in every mode; the choice is a cost choice.
+enum { KM_SCREEN_X3 = 0, KM_SCREEN_X3_REFINE = 1, KM_SCREEN_FAST1 = 2, KM_SCREEN_FAST2 = 3 };
+bool fast_path_ok(const Geometry& g);
+// C32, cmax: fp32 centroids and max norm (fast screen image); bal: 2 floats of
+// scratch (fast screen image error maxima)
 hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, const _Float16* Chi,
                         const _Float16* Clo, uint4* ChiF, uint4* CloF, const float* cn2s, const float* bnd,
                         const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,
-                        double* stats, int with_stats, int refine, int n_cu, QLayout* ql, const int* gate,
-                        hipStream_t s);
+                        double* stats, int with_stats, int mode, int n_cu, QLayout* ql, const int* gate,
+                        hipStream_t s, const float* C32, const float* cmax, float* bal);
 hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float* cabs, int dp, float* bnd,
                                const int* gate, hipStream_t s);
 hipError_t launch_row_norm(const float* X, const Geometry& g, float* xnorm, hipStream_t s);

@@ -1258,9 +1258,10 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   static_assert(B >= 3 && B - 2 <= 12, "index bits");
   static_assert(NB >= 2, "pipelined blocks");
   constexpr uint32_t maskq = (1u << (B - 2)) - 1u;
+  constexpr int TS = KP;  // sum table row stride (KP + 2, which moves the lane halves to opposite bank halves: no gain)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* sCn = reinterpret_cast<float*>(smem);                  // ||c||^2 s^2 [KP]
-  double* tab = reinterpret_cast<double*>(smem + KP * 4);        // [DP][KP]
+  double* tab = reinterpret_cast<double*>(smem + KP * 4);        // [DP + 1][TS]
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -1268,7 +1269,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   const int h = lane >> 5;
   for (int i = threadIdx.x; i < KP; i += WAVES * 64) sCn[i] = A.cn2s[i];
   if constexpr (STATS)
-    for (int i = threadIdx.x; i < (DP + 1) * KP; i += WAVES * 64) tab[i] = 0.0;
+    for (int i = threadIdx.x; i < (DP + 1) * TS; i += WAVES * 64) tab[i] = 0.0;
   f16x8 Ahi[NB][NS], Alo[NB][NS];
 #pragma unroll
   for (int b = 0; b < NB; ++b)
@@ -1452,13 +1453,13 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       const int lab = (int)(__float_as_uint(a1[0] + a1[1] + a1[2] + a1[3] + a2[0] + a2[1] + a2[2] + a2[3] + xn) & 255u) % A.k;
       if (h == 0 && valid) A.labels[row] = lab;
       if constexpr (STATS) {
-        double* tp = tab + (size_t)(8 * h) * KP + lab;
+        double* tp = tab + (size_t)(8 * h) * TS + lab;
 #pragma unroll
         for (int t = 0; t < NS; ++t) {
           const float4 v0 = xc[t][0], v1 = xc[t][1];
           const float xe[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-          for (int e = 0; e < 8; ++e) atomicAdd(tp + (size_t)(16 * t + e) * KP, (double)xe[e]);
+          for (int e = 0; e < 8; ++e) atomicAdd(tp + (size_t)(16 * t + e) * TS, (double)xe[e]);
         }
       }
       return;
@@ -1570,15 +1571,15 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
     }
     if constexpr (STATS && ABL != 3) {
       if (valid && kind == 0) {
-        double* tp = tab + (size_t)(8 * h) * KP + lab;
+        double* tp = tab + (size_t)(8 * h) * TS + lab;
 #pragma unroll
         for (int t = 0; t < NS; ++t) {
           const float4 v0 = xc[t][0], v1 = xc[t][1];
           const float xe[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-          for (int e = 0; e < 8; ++e) atomicAdd(tp + (size_t)(16 * t + e) * KP, (double)xe[e]);
+          for (int e = 0; e < 8; ++e) atomicAdd(tp + (size_t)(16 * t + e) * TS, (double)xe[e]);
         }
-        if (h == 0) atomicAdd(tab + (size_t)DP * KP + lab, 1.0);  // count row
+        if (h == 0) atomicAdd(tab + (size_t)DP * TS + lab, 1.0);  // count row
       }
     }
     if constexpr (ABL == 7) {
@@ -1622,7 +1623,417 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
     for (int i = threadIdx.x; i < (DP + 1) * KP; i += WAVES * 64) {
       const int j = i / (DP + 1);
       const int f = i - j * (DP + 1);
-      const double v = tab[(size_t)f * KP + j];
+      const double v = tab[(size_t)f * TS + j];
+      if (v != 0.0 && (f < A.d || f == DP) && j < A.k) atomicAdd(A.stats + (size_t)j * d1 + (f == DP ? A.d : f), v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fast screen (k_fused1): ONE fp16 image of -2cs (128 AGPRs instead of 256)
+// against the row as one fp16 part (NX = 1: one MFMA per product instead of
+// three) or hi + lo (NX = 2), with a PAIRWISE error bound (DESIGN.md §2 "Fast
+// screen").  The image is rounded per feature to either fp16 neighbour of
+// a = -2 c' (c' = c32 s), chosen so that alpha . c' ~ 0 (alpha = image - a).
+// For a point X (scaled row) and centroids j, i, the screen errors satisfy
+//   |E_j - E_i| <= C0 + c (D_j + D_i),   D_j = ||X - c'_j||,
+//   c  = 2 ||beta|| + max ||alpha||            (beta: row rounding, <= u16 ||X||)
+//   C0 = 2 Acc + 2 nu + 4 u24 cm xn + 2 max |alpha . c'| + 2 max||alpha|| ||beta||
+// since  E_j = acc_j + nu_j - 2 gamma_j.X - 2 c'_j.beta + alpha_j.X + alpha_j.beta
+// with alpha_j.X = alpha_j.c'_j + alpha_j.(X - c'_j): the errors that matter
+// for a decision scale with the DISTANCES to the two centroids, not with
+// ||c|| ||x|| as in a global bound.  D_j is bounded from the key itself.
+// ---------------------------------------------------------------------------
+
+// one fp16 step from h towards +inf (up) or -inf
+__device__ __forceinline__ _Float16 f16_step(_Float16 h, bool up) {
+  uint16_t b = __builtin_bit_cast(uint16_t, h);
+  if ((b & 0x7fffu) == 0u) return __builtin_bit_cast(_Float16, (uint16_t)(up ? 0x0001u : 0x8001u));
+  const bool neg = (b & 0x8000u) != 0u;
+  b = (up != neg) ? (uint16_t)(b + 1u) : (uint16_t)(b - 1u);
+  return __builtin_bit_cast(_Float16, b);
+}
+
+// Balanced image, written fragment-linear (piece (b, t), lane l, 8 halves:
+// the k_frag_images layout), one thread per centroid: a greedy pass over the
+// features picks the neighbour that keeps the running alpha . c' smallest,
+// then two passes of single flips that shrink it.  bal[0] = max_j ||alpha_j||,
+// bal[1] = max_j |alpha_j . c'_j| (scaled units, rounded up; real centroids).
+__global__ __launch_bounds__(512) void k_prep_bal(const float* __restrict__ C32, int k, int kp, int dp,
+                                                  const float* __restrict__ xabs, const float* __restrict__ cabs,
+                                                  uint16_t* __restrict__ imgF, float* __restrict__ bal,
+                                                  const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
+  __shared__ float red[2][8];
+  const float s = mfma_scale(*xabs, *cabs);
+  const int ns = dp / 16;
+  float an = 0.0f, ac = 0.0f;
+  for (int j = threadIdx.x; j < kp; j += blockDim.x) {
+    const float* cr = C32 + (size_t)j * dp;
+    auto at = [&](int f) -> uint16_t& {
+      const int b = j >> 5, t = f >> 4, l = (j & 31) + 32 * ((f >> 3) & 1);
+      return imgF[((size_t)((b * ns + t) * 64 + l)) * 8 + (f & 7)];
+    };
+    // alpha_f c'_f for image value v (exact in float64: both factors <= 24 bits)
+    auto err = [&](_Float16 v, float a) { return ((double)(float)v - (double)a) * (-0.5 * (double)a); };
+    double run = 0.0;
+    for (int f = 0; f < dp; ++f) {
+      const float a = -2.0f * cr[f] * s;
+      const _Float16 h = (_Float16)a;
+      const _Float16 o = ((float)h == a) ? h : f16_step(h, a > (float)h);
+      const double eh = err(h, a), eo = err(o, a);
+      const bool po = fabs(run + eo) < fabs(run + eh);
+      run += po ? eo : eh;
+      at(f) = __builtin_bit_cast(uint16_t, po ? o : h);
+    }
+    for (int pass = 0; pass < 2; ++pass)
+      for (int f = 0; f < dp; ++f) {
+        const float a = -2.0f * cr[f] * s;
+        const _Float16 h = (_Float16)a;
+        const _Float16 o = ((float)h == a) ? h : f16_step(h, a > (float)h);
+        const _Float16 cur = __builtin_bit_cast(_Float16, at(f));
+        const _Float16 alt = (__builtin_bit_cast(uint16_t, cur) == __builtin_bit_cast(uint16_t, h)) ? o : h;
+        const double ec = err(cur, a), ea = err(alt, a);
+        if (fabs(run - ec + ea) < fabs(run)) {
+          run = run - ec + ea;
+          at(f) = __builtin_bit_cast(uint16_t, alt);
+        }
+      }
+    // exact recount of both maxima from the stored image
+    double nn = 0.0, sum = 0.0, sabs = 0.0;
+    for (int f = 0; f < dp; ++f) {
+      const float a = -2.0f * cr[f] * s;
+      const _Float16 v = __builtin_bit_cast(_Float16, at(f));
+      const double al = (double)(float)v - (double)a;
+      nn += al * al;
+      const double e = err(v, a);
+      sum += e;
+      sabs += fabs(e);
+    }
+    if (j < k) {
+      const double nb = sqrt(nn) * (1.0 + 1e-12);
+      const double cb = fabs(sum) + (double)dp * 2.3e-16 * sabs;  // float64 summation slack
+      an = fmaxf(an, (float)nb * (1.0f + 2.0f * U24));
+      ac = fmaxf(ac, (float)cb * (1.0f + 2.0f * U24) + 1e-30f);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    an = fmaxf(an, __shfl_xor(an, o));
+    ac = fmaxf(ac, __shfl_xor(ac, o));
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wave] = an;
+    red[1][wave] = ac;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m0 = 0.0f, m1 = 0.0f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+      m0 = fmaxf(m0, red[0][w]);
+      m1 = fmaxf(m1, red[1][w]);
+    }
+    bal[0] = m0;
+    bal[1] = m1;
+  }
+}
+
+// NX = 1: the row as one fp16 part; NX = 2: hi + lo (the image stays one part).
+// bal = {max ||alpha||, max |alpha . c'|} from k_prep_bal; cmaxp = max ||c|| (unscaled)
+template <int NS, int NB, int NX, bool STATS, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_fused1(FusedArgs A, const float* __restrict__ bal,
+                                                          const float* __restrict__ cmaxp) {
+  if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
+  constexpr int DP = 16 * NS;
+  constexpr int KP = 32 * NB;
+  constexpr int B = ceil_log2_c(KP);
+  static_assert(B >= 3 && B - 2 <= 12, "index bits");
+  static_assert(NB >= 2, "pipelined blocks");
+  static_assert(NX == 1 || NX == 2, "row parts");
+  constexpr uint32_t maskq = (1u << (B - 2)) - 1u;
+  constexpr int TS = KP;  // sum table row stride (KP + 2, which moves the lane halves to opposite bank halves: no gain)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* sCn = reinterpret_cast<float*>(smem);                  // ||c||^2 s^2 [KP]
+  double* tab = reinterpret_cast<double*>(smem + KP * 4);        // [DP + 1][TS]
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  for (int i = threadIdx.x; i < KP; i += WAVES * 64) sCn[i] = A.cn2s[i];
+  if constexpr (STATS)
+    for (int i = threadIdx.x; i < (DP + 1) * TS; i += WAVES * 64) tab[i] = 0.0;
+  f16x8 Ahi[NB][NS];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int t = 0; t < NS; ++t) Ahi[b][t] = __builtin_bit_cast(f16x8, A.ChiF[(b * NS + t) * 64 + lane]);
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int t = 0; t < NS; ++t) asm volatile("" : "+a"(Ahi[b][t]));
+  __syncthreads();
+
+  const float s = mfma_scale(*A.xabs, *A.cabs);
+  // pairwise-bound constants (scaled units), every per-point term affine in
+  // xn = s ||x|| (per-row upper bound)
+  const float cm = *cmaxp * s;
+  const float pm = (*A.cabs * s) * (*A.xabs * s) * 1.0001f;
+  const float sq = sqrtf((float)DP);
+  // fp16 subnormals (flushed or not): 2^-14 per element, on row and image
+  // (|alpha_f| grows by <= 2^-14 only where |c'_f| < 2^-15)
+  const float an = bal[0] + 6.103515625e-05f * sq, ac = bal[1] + (float)DP * 1.862645149230957e-09f;
+  constexpr float NM = (float)(NX * NS);  // MFMAs per score chain
+  // ||beta|| <= bq1 xn + bq0 (row rounding: u16 = 2^-11; hi + lo: u16^2)
+  const float bq1 = (NX == 1 ? 4.8828125e-4f : 2.384185791015625e-07f) * 1.0001f;
+  const float bq0 = 6.103515625e-05f * sq;
+  // accumulation (one rounding of |D| <= cm^2 + 2 cm xn per MFMA, and the
+  // in-group alignment truncation, 14 u24 x the largest product 2 pm)
+  const float acc1 = NM * U24 * 2.01f * cm;
+  const float acc0 = NM * U24 * (cm * cm + 28.1f * pm);
+  const float nu = 1.01f * U24 * cm * cm;  // ||c||^2 s^2 rounding
+  // |E_j| <= G = Acc + nu + 2 u24 cm xn + 2 cm ||beta|| + max||alpha|| (xn + ||beta||)
+  const float G1 = acc1 + 2.01f * U24 * cm + 2.01f * cm * bq1 + an * (1.0f + bq1);
+  const float G0 = acc0 + nu + 2.01f * cm * bq0 + an * bq0;
+  const float c1 = 2.0f * bq1, c0 = 2.0f * bq0 + an * 1.0001f;
+  const float h1 = 2.0f * acc1 + 4.01f * U24 * cm + 2.0f * an * bq1;
+  const float h0 = 2.0f * acc0 + 2.0f * nu + 2.0f * ac + 2.0f * an * bq0;
+  // key truncation (index bits) plus the rounding of a key difference
+  const float rho2 = __builtin_ldexpf(1.0f, B - 2 - 23) * 1.01f + 2.0f * U24;
+
+  const int64_t n = A.n;
+  const int64_t ntiles = (n + 31) / 32;
+  const uint32_t gw = blockIdx.x * WAVES + wave;
+  QEntry* wq = A.queue + (size_t)gw * A.seg;
+  uint32_t qn = 0, qf = 0;
+  const int64_t tstride = (int64_t)gridDim.x * WAVES;
+  const float4* cnl = reinterpret_cast<const float4*>(sCn + 4 * h);  // + 8 blk + 2 g4
+
+  auto load_tile = [&](int64_t tile, float4 (&xq)[NS][2], float& xnq) {
+    const int64_t row = tile * 32 + r;
+    const int64_t rr = row < n ? row : (n - 1);
+    const float* xr = A.X + rr * DP + 8 * h;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      xq[t][0] = *reinterpret_cast<const float4*>(xr + 16 * t);
+      xq[t][1] = *reinterpret_cast<const float4*>(xr + 16 * t + 4);
+    }
+    xnq = A.xnorm[rr];
+  };
+
+  auto process_tile = [&](int64_t tile, const float4 (&xc)[NS][2], float xn) {
+    const int64_t row = tile * 32 + r;
+    const bool valid = row < n;
+    // B operand: lane (r, h) holds features [16t + 8h, +8) of point r
+    f16x8 bh[NS], bl[NS];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      const float xv[8] = {xc[t][0].x, xc[t][0].y, xc[t][0].z, xc[t][0].w,
+                           xc[t][1].x, xc[t][1].y, xc[t][1].z, xc[t][1].w};
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const float xs0 = xv[e] * s, xs1 = xv[e + 1] * s;
+        const f16x2 hp = {(_Float16)xs0, (_Float16)xs1};
+        bh[t][e] = hp[0];
+        bh[t][e + 1] = hp[1];
+        if constexpr (NX == 2) {
+          uint32_t lp;
+          asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
+              "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+              : "=&v"(lp)
+              : "v"(__builtin_bit_cast(uint32_t, hp)), "v"(xs0), "v"(xs1));
+          const f16x2 lo = __builtin_bit_cast(f16x2, lp);
+          bl[t][e] = lo[0];
+          bl[t][e + 1] = lo[1];
+        }
+      }
+    }
+    float a1[4], a2[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a1[c] = a2[c] = FLT_MAX;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int t = 0; t < NS; ++t) asm volatile("" : "+a"(Ahi[b][t]));
+    auto cn_init = [&](int blk) {
+      f32x16 acc;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 cv = cnl[8 * blk + 2 * g4];
+        acc[4 * g4 + 0] = cv.x;
+        acc[4 * g4 + 1] = cv.y;
+        acc[4 * g4 + 2] = cv.z;
+        acc[4 * g4 + 3] = cv.w;
+      }
+      return acc;
+    };
+    auto mfma_block = [&](f32x16 acc, int blk) {
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+        if constexpr (NX == 2) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bl[t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bh[t], acc, 0, 0, 0);
+      }
+      return acc;
+    };
+    // register reg holds centroid j = 32 blk + 4h + (reg & 3) + 8 (reg >> 2);
+    // chain reg & 3 keeps the top two keys (score | j >> 2) (as in k_fused)
+    auto keys_block = [&](const f32x16& acc, int blk) {
+      const uint32_t jq = (uint32_t)(8 * blk + h);
+#pragma unroll
+      for (int q = 0; q < 16; q += 8)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int ra = q + c, rb = q + c + 4;
+          const float ka = __uint_as_float((__float_as_uint(acc[ra]) & ~maskq) | (jq | (uint32_t)(2 * (ra >> 2))));
+          const float kb = __uint_as_float((__float_as_uint(acc[rb]) & ~maskq) | (jq | (uint32_t)(2 * (rb >> 2))));
+          const float t = __builtin_amdgcn_fmed3f(a1[c], ka, kb);
+          a1[c] = __builtin_fminf(__builtin_fminf(a1[c], ka), kb);
+          a2[c] = __builtin_fminf(a2[c], t);
+        }
+    };
+    constexpr int NMB = NX * NS;  // MFMAs per block
+    f32x16 accs[2];
+    f32x16 cinit = cn_init(1);
+    accs[0] = mfma_block(cn_init(0), 0);
+#pragma unroll
+    for (int blk = 1; blk < NB; ++blk) {
+      const f32x16 cin = cinit;
+      if (blk + 1 < NB) cinit = cn_init(blk + 1);
+      accs[blk & 1] = mfma_block(cin, blk);
+      keys_block(accs[(blk - 1) & 1], blk - 1);
+      // MFMA, next block's init reads, then (VALU x m, MFMA) pairs
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+      for (int i = 0; i < NMB - 1; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x2, 40 / NMB + 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    keys_block(accs[(NB - 1) & 1], NB - 1);
+
+    auto pidx = [&](float key, int c) { return ((__float_as_uint(key) & maskq) << 2) | (uint32_t)c; };
+    float k1 = a1[0], k2 = a2[0], k3 = a2[0];
+    uint32_t p1 = pidx(a1[0], 0), p2 = pidx(a2[0], 0);
+    {
+      float m1 = a1[2], m2 = a2[2], m3 = a2[2];
+      uint32_t q1 = pidx(a1[2], 2), q2 = pidx(a2[2], 2);
+      merge3(k1, k2, k3, p1, p2, a1[1], a2[1], a2[1], pidx(a1[1], 1), pidx(a2[1], 1));
+      merge3(m1, m2, m3, q1, q2, a1[3], a2[3], a2[3], pidx(a1[3], 3), pidx(a2[3], 3));
+      merge3(k1, k2, k3, p1, p2, m1, m2, m3, q1, q2);
+    }
+    {
+      uint32_t K1, Q1, K2, Q2, K3, Q3, P1, R1, P2, R2;
+      perm_halves(__float_as_uint(k1), K1, Q1);
+      perm_halves(__float_as_uint(k2), K2, Q2);
+      perm_halves(__float_as_uint(k3), K3, Q3);
+      perm_halves(p1, P1, R1);
+      perm_halves(p2, P2, R2);
+      k1 = __uint_as_float(K1);
+      k2 = __uint_as_float(K2);
+      k3 = __uint_as_float(K3);
+      p1 = P1;
+      p2 = P2;
+      merge3(k1, k2, k3, p1, p2, __uint_as_float(Q1), __uint_as_float(Q2), __uint_as_float(Q3), R1, R2);
+    }
+    const bool same_chain = ((p1 ^ p2) & 7u) == 0u;
+    // pairwise test of the best against every key >= kj
+    const float xs = xn * s;
+    const float G = fmaf(G1, xs, G0), cs = fmaf(c1, xs, c0), C0 = fmaf(h1, xs, h0);
+    const float x2 = xs * xs;
+    const float mono = 1.01f * cs + U24 * cm;
+    // D(K): upper bound of ||X - c'_j|| for a centroid with key K
+    auto Dof = [&](float K) {
+      const float Kp = K + rho2 * fabsf(K);
+      const float arg = Kp + G + x2 + 4.0f * U24 * (fabsf(Kp) + G + x2);
+      return sqrtf(fmaxf(arg, 0.0f)) * (1.0f + 4.0f * U24) + U24 * cm;
+    };
+    const float D1 = Dof(k1);
+    // every centroid with key >= kj is provably farther than the best: the
+    // gap beats the pair bound at kj, and the gap grows faster than the bound
+    // beyond kj (d/dK of c D(K) < 1/2 once D >= 1.01 c)
+    auto sep = [&](float kj) {
+      const float Dj = Dof(kj);
+      const float gap = (kj - k1) - rho2 * (fabsf(k1) + fabsf(kj));
+      const float P = fmaf(cs, D1 + Dj, C0) * 1.0002f;
+      return gap > P && Dj >= mono;
+    };
+    uint32_t kind = 0;
+    if (!sep(k2)) kind = (same_chain || !sep(k3)) ? 2u : 1u;
+    // p1, p2 in one chain but every other chain's best separated: scan only
+    // that chain (kind 3), as in k_fused
+    if (__ballot(kind == 2u && same_chain) != 0ull) {
+      const uint32_t cs8 = p1 & 7u;
+      float o = FLT_MAX;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t v0, v1;
+        perm_halves(__float_as_uint(a1[c]), v0, v1);
+        if ((uint32_t)c != cs8) o = kmin(o, __uint_as_float(v0));
+        if ((uint32_t)(4 + c) != cs8) o = kmin(o, __uint_as_float(v1));
+      }
+      if (kind == 2u && same_chain && sep(o)) kind = 3u;
+    }
+    const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
+    if (h == 0 && valid) A.labels[row] = lab;
+    const bool enq = (h == 0) && valid && (kind != 0);
+    const uint64_t m = __ballot(enq);
+    if (m) {
+      const uint64_t m1 = __ballot(enq && kind == 1);
+      const uint64_t m2 = m & ~m1;
+      const uint64_t below = (1ull << lane) - 1ull;
+      if (enq) {
+        QEntry q;
+        q.row = (uint32_t)row;
+        q.i1 = p1;
+        q.i2 = p2;
+        q.kind = kind;
+        const uint32_t pos = (kind == 1) ? qn + (uint32_t)__popcll(m1 & below)
+                                         : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
+        wq[pos] = q;
+      }
+      qn += (uint32_t)__popcll(m1);
+      qf += (uint32_t)__popcll(m2);
+    }
+    if constexpr (STATS) {
+      if (valid && kind == 0) {
+        double* tp = tab + (size_t)(8 * h) * TS + lab;
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+          const float4 v0 = xc[t][0], v1 = xc[t][1];
+          const float xe[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) atomicAdd(tp + (size_t)(16 * t + e) * TS, (double)xe[e]);
+        }
+        if (h == 0) atomicAdd(tab + (size_t)DP * TS + lab, 1.0);  // count row
+      }
+    }
+  };
+
+  float4 xb0[NS][2], xb1[NS][2];
+  float xn0 = 0.0f, xn1 = 0.0f;
+  load_tile(gw, xb0, xn0);
+  for (int64_t tile = gw; tile < ntiles; tile += 2 * tstride) {
+    const int64_t t1 = tile + tstride;
+    load_tile(t1, xb1, xn1);
+    process_tile(tile, xb0, xn0);
+    if (t1 >= ntiles) break;
+    load_tile(t1 + tstride, xb0, xn0);
+    process_tile(t1, xb1, xn1);
+  }
+  if (lane == 0) {
+    A.qcount[2 * gw] = qn;
+    A.qcount[2 * gw + 1] = qf;
+  }
+  if constexpr (STATS) {
+    __syncthreads();
+    const int d1 = A.d + 1;
+    for (int i = threadIdx.x; i < (DP + 1) * KP; i += WAVES * 64) {
+      const int j = i / (DP + 1);
+      const int f = i - j * (DP + 1);
+      const double v = tab[(size_t)f * TS + j];
       if (v != 0.0 && (f < A.d || f == DP) && j < A.k) atomicAdd(A.stats + (size_t)j * d1 + (f == DP ? A.d : f), v);
     }
   }
@@ -1731,15 +2142,45 @@ bool fused_path_ok(const Geometry& g) {
   }
 }
 
+bool fast_path_ok(const Geometry& g) { return g.dp == 64 && g.kp == 256; }
+
 hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, const _Float16* Chi,
                         const _Float16* Clo, uint4* ChiF, uint4* CloF, const float* cn2s, const float* bnd,
                         const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,
-                        double* stats, int with_stats, int refine, int n_cu, QLayout* ql, const int* gate,
-                        hipStream_t s) {
+                        double* stats, int with_stats, int mode, int n_cu, QLayout* ql, const int* gate,
+                        hipStream_t s, const float* C32, const float* cmax, float* bal) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
   const int ns = g.dp / 16, nb = g.kp / 32;
+  const int refine = (mode == KM_SCREEN_X3_REFINE) ? 1 : 0;
+  if ((mode == KM_SCREEN_FAST1 || mode == KM_SCREEN_FAST2) && fast_path_ok(g)) {
+    hipLaunchKernelGGL(k_prep_bal, dim3(1), dim3(512), 0, s, C32, g.k, g.kp, g.dp, xabs, cabs,
+                       reinterpret_cast<uint16_t*>(ChiF), bal, gate);
+    constexpr int WAVES = 4;
+    const int64_t ntiles = (g.n + 31) / 32;
+    int64_t blocks = n_cu;
+    if (blocks > (ntiles + WAVES - 1) / WAVES) blocks = (ntiles + WAVES - 1) / WAVES;
+    const int nbk = (int)blocks;
+    const int64_t nw = (int64_t)nbk * WAVES;
+    const uint32_t seg = (uint32_t)(((ntiles + nw - 1) / nw) * 32);
+    ql->seg = seg;
+    ql->nwaves = (uint32_t)nw;
+    FusedArgs a{X, xnorm, g.n, g.k, g.d, seg, ChiF, CloF, cn2s, bnd, xabs, cabs, labels, queue, qcount, stats, gate};
+    const size_t lds = (size_t)g.kp * 4 + (with_stats ? (size_t)(g.dp + 1) * g.kp * 8 : 0);
+    if (mode == KM_SCREEN_FAST1) {
+      if (with_stats)
+        hipLaunchKernelGGL((k_fused1<4, 8, 1, true, WAVES>), dim3(nbk), dim3(WAVES * 64), lds, s, a, bal, cmax);
+      else
+        hipLaunchKernelGGL((k_fused1<4, 8, 1, false, WAVES>), dim3(nbk), dim3(WAVES * 64), lds, s, a, bal, cmax);
+    } else {
+      if (with_stats)
+        hipLaunchKernelGGL((k_fused1<4, 8, 2, true, WAVES>), dim3(nbk), dim3(WAVES * 64), lds, s, a, bal, cmax);
+      else
+        hipLaunchKernelGGL((k_fused1<4, 8, 2, false, WAVES>), dim3(nbk), dim3(WAVES * 64), lds, s, a, bal, cmax);
+    }
+    return hipGetLastError();
+  }
   {
     const int total = nb * ns * 64;
     hipLaunchKernelGGL(k_frag_images, dim3((total + 255) / 256), dim3(256), 0, s, Chi, Clo, g.kp, g.dp, ChiF, CloF, gate);

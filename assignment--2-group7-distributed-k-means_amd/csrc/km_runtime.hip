@@ -73,11 +73,19 @@ struct km_ctx {
   bool have_c = false;
   int path = 0;  // 1 small, 2 mfma
   bool fused = false;  // path 2 with the fused assign + sums kernel
-  // k_fused with per-key bound refinement: on for the first iteration after
-  // new centroids, then while more than 1/64 of this rank's rows queue for
-  // exact resolution (the refinement costs ~4% where the global test settles
-  // nearly every row, and saves most of the exact work where it does not)
-  bool refine = true;
+  // screen of the fused kernel (km::KM_SCREEN_*), a cost choice (results are
+  // exact in every mode), made per batch from the last iteration's queue:
+  // fp16x3 with the per-key refinement for the first iteration after new
+  // centroids and while more than 1/64 of this rank's rows queue for exact
+  // resolution (the refinement costs ~4% where the global test settles
+  // nearly every row, and saves most of the exact work where it does not);
+  // the fast screen (one fp16 MFMA per product, pairwise bound: 13% less
+  // kernel time at c3, ~15-20x the queue) once fewer than 1/2048 of the rows
+  // queue, unless it queued more than 1/128 since the last new centroids
+  int screen = km::KM_SCREEN_X3_REFINE;
+  bool fast_blocked = false;
+  int screen_forced = -1;  // km_set_screen: a fixed mode, or -1 (the policy above)
+  float* bal = nullptr;  // fast screen: image error maxima (2 floats)
   // statistics already zero (the batch update cleared them): no memset
   bool stats_clean = false;
   // device repair kernels enqueued in batches: armed for the first batch
@@ -203,6 +211,7 @@ void free_centroids(km_ctx* c) {
   dfree(c->ChiF);
   dfree(c->CloF);
   dfree(c->bnd);
+  c->bal = nullptr;
   dfree(c->cmax);
   dfree(c->cabs);
   dfree(c->stats_own);
@@ -327,9 +336,9 @@ int run_assign(km_ctx* c, bool with_stats) {
     {
       ProfScope ps(c, KM_K_ASSIGN);
       KM_HIP(km::launch_fused(c->X, c->xnorm, g, c->Chi, c->Clo, c->ChiF, c->CloF, c->cn2s, c->bnd, c->xabs, c->cabs,
-                              c->labels, c->queue, c->qcount, c->stats, with_stats ? 1 : 0, (c->refine || !with_stats) ? 1 : 0,
-                              c->n_cu, &c->ql,
-                              c->gate, c->stream));
+                              c->labels, c->queue, c->qcount, c->stats, with_stats ? 1 : 0,
+                              (with_stats || c->screen >= km::KM_SCREEN_FAST1) ? c->screen : km::KM_SCREEN_X3_REFINE,
+                              c->n_cu, &c->ql, c->gate, c->stream, c->C32, c->cmax, c->bal));
     }
     {
       ProfScope ps(c, KM_K_RESOLVE);
@@ -565,6 +574,20 @@ int km_sum_x(km_ctx* c, double* out) {
   return KM_OK;
 }
 
+int km_set_screen(km_ctx* c, int32_t mode) {
+  KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
+  KM_REQUIRE(mode >= -1 && mode <= km::KM_SCREEN_FAST2, KM_ERR_ARG, "km_set_screen: mode must be -1..3");
+  c->screen_forced = mode;
+  if (mode >= 0) c->screen = mode;
+  return KM_OK;
+}
+
+int km_get_screen(km_ctx* c, int32_t* mode) {
+  KM_REQUIRE(c && mode, KM_ERR_ARG, "null ctx");
+  *mode = c->screen;
+  return KM_OK;
+}
+
 int km_set_sse(km_ctx* c, int32_t enable) {
   KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
   c->want_sse = enable != 0;
@@ -598,6 +621,7 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
     KM_HIP(hipMalloc(&c->ChiF, sizeof(_Float16) * kp * dp));
     KM_HIP(hipMalloc(&c->CloF, sizeof(_Float16) * kp * dp));
     KM_HIP(hipMalloc(&c->bnd, sizeof(float) * 4));
+    c->bal = c->bnd + 2;  // [0, 1]: screening-bound constants, [2, 3]: fast screen image maxima
     KM_HIP(hipMalloc(&c->cmax, sizeof(float)));
     KM_HIP(hipMalloc(&c->cabs, sizeof(float)));
     KM_HIP(hipMalloc(&c->stats_own, sizeof(double) * stats_len(c->g)));
@@ -626,7 +650,8 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
   if (rc != KM_OK) return rc;
   KM_HIP(hipStreamSynchronize(c->stream));
   c->have_c = true;
-  c->refine = true;
+  c->screen = c->screen_forced >= 0 ? c->screen_forced : km::KM_SCREEN_X3_REFINE;
+  c->fast_blocked = false;
   c->rep_armed = c->rep_enabled;
   return KM_OK;
 }
@@ -662,8 +687,23 @@ int km_bind_stats_buffer(km_ctx* c, void* p) {
   return KM_OK;
 }
 
+static int fast_mode() {
+  static const int m = km::diag_env("KM_FAST", 1);  // diagnostic build: 0 off, 1 / 2 row parts
+  return m == 0 ? -1 : (m == 2 ? km::KM_SCREEN_FAST2 : km::KM_SCREEN_FAST1);
+}
+
 static void note_queue(km_ctx* c, const km::DevStatus& s) {
-  c->refine = ((int64_t)s.q_rerank + s.q_full) * 64 > c->g.n;
+  if (c->screen_forced >= 0) return;
+  const int64_t q = (int64_t)s.q_rerank + s.q_full;
+  const bool was_fast = c->screen >= km::KM_SCREEN_FAST1;
+  if (was_fast && q * 128 > c->g.n) c->fast_blocked = true;
+  if (was_fast && !c->fast_blocked) return;
+  if (q * 64 > c->g.n && !was_fast)
+    c->screen = km::KM_SCREEN_X3_REFINE;
+  else if (!was_fast && q * 2048 < c->g.n && !c->fast_blocked && fast_mode() >= 0 && km::fast_path_ok(c->g))
+    c->screen = fast_mode();
+  else
+    c->screen = km::KM_SCREEN_X3;
 }
 
 int km_update(km_ctx* c, km_status* st, int64_t* counts) {
@@ -849,7 +889,8 @@ int km_replace_rows(km_ctx* c, const int32_t* ids, const double* rows, int32_t n
   KM_HIP(hipSetDevice(c->device));
   if (n == 0) return KM_OK;
   if (c->prep_of == c->C64_new) c->prep_of = nullptr;  // its images are stale now
-  c->refine = true;
+  c->screen = c->screen_forced >= 0 ? c->screen_forced : km::KM_SCREEN_X3_REFINE;
+  c->fast_blocked = false;
   c->rep_armed = c->rep_enabled;
   std::vector<int64_t> ids64(n);
   for (int i = 0; i < n; ++i) {

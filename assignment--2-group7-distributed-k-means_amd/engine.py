@@ -98,6 +98,18 @@ class HipEngine:
         SSE slot during assign_stats (kmeans_spark.py:278-286)."""
         self._c(self.lib.km_set_sse(self.ctx, 1 if enable else 0), "km_set_sse")
 
+    def set_screen(self, mode: int) -> None:
+        """Screening kernel of the fused path (-1 auto; 0 fp16x3; 1 fp16x3 +
+        per-key bounds; 2 fast fp16 screen; 3 fast, row hi + lo).  A cost
+        choice only: results are exact in every mode (tests pin each one)."""
+        self._c(self.lib.km_set_screen(self.ctx, int(mode)), "km_set_screen")
+
+    def screen(self) -> int:
+        """The screen the next fused launch uses (0..3)."""
+        m = ctypes.c_int32()
+        self._c(self.lib.km_get_screen(self.ctx, ctypes.byref(m)), "km_get_screen")
+        return m.value
+
     # -- centroids / iteration -------------------------------------------------
     def set_centroids(self, C: np.ndarray) -> None:
         C = np.ascontiguousarray(C, dtype=np.float64)

@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--screen", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
+                   help="fused-path screen (km_set_screen): -1 the runtime's per-batch choice")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work per worker")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="per-launch HBM bytes from a rocprofv3 --pmc pass (optional)")
@@ -147,6 +149,7 @@ def main():
     if args.config in POOR_SEEDS:
         C0 = np.vstack([C0[:3], np.full((k - 3, d), 100.0) + np.arange(k - 3)[:, None]])
     eng = run.engine
+    eng.set_screen(args.screen)
     eng.set_centroids(C0)
     km.sse_history = []
 
@@ -184,6 +187,7 @@ def main():
 
     kern = {name: eng.prof_read(name) for name in ("assign", "resolve", "stats", "update", "prep")}
     info = eng.info()
+    screen = eng.screen() if info["fused_stats"] and info["path"] == 2 else None
     n_local = info["n"]
     flops_launch = 2.0 * n_local * k * d                 # algorithmic distance contraction
     bytes_stats = n_local * (d * 4 + 4)                  # X once + labels
@@ -200,7 +204,27 @@ def main():
                 traffic = tj.get("bytes_per_launch") * n_local / N
         except Exception:
             traffic = None
-    if info["path"] == 2 and dom == "assign":
+    if info["path"] == 2 and dom == "assign" and screen in (2, 3):
+        # fast screen: NX fp16 MFMAs per product (2516.6 TF dense) -- at c3 the
+        # MFMA time is 1.3 ms (NX = 1) against 3.2 ms of HBM, so HBM bounds it
+        nx = 1 if screen == 2 else 2
+        t_mfma = flops_launch * nx / (F16_DENSE_TFLOPS * 1e12)
+        bytes_fast = n_local * (d * 4 + 8)               # X once + row norm + label
+        t_hbm = bytes_fast / (HBM_PEAK_GBS * 1e9)
+        kname = f"k_fused1 (fast fp16 screen, {nx} row part{'s' if nx > 1 else ''}, pairwise bound + f64 sums)"
+        if t_hbm >= t_mfma:
+            ach = bytes_fast / avg_s / 1e9
+            roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                    "traffic": traffic, "kernel": kname,
+                    "bytes_note": "N*(d*4+8) per launch (rows once + row norm + label); the MFMA time at "
+                                  f"{nx} fp16 MFMA(s) per product is {t_mfma * 1e3:.2f} ms vs {t_hbm * 1e3:.2f} ms HBM",
+                    "tflops": flops_launch / avg_s / 1e12}
+        else:
+            ach = flops_launch * nx / avg_s / 1e12
+            roof = {"bound": "mfma", "achieved": ach, "peak": F16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                    "frac": ach / F16_DENSE_TFLOPS, "traffic": traffic, "kernel": kname,
+                    "peak_note": f"dense f16 MFMA 2516.6 TF; achieved = {nx}*2*n*k*d per launch / avg launch time"}
+    elif info["path"] == 2 and dom == "assign":
         ach = flops_launch / avg_s / 1e12
         kname = ("k_fused (fp16x3 screen + f64 sums)" if info["fused_stats"] else
                  "k_assign_wide (fp16x3 screen, feature chunks)" if info["dp"] > 256 else
@@ -230,8 +254,10 @@ def main():
             "points_per_sec": N * it_s, "roofline": roof, "kernel_avg_ms": kernel_ms,
             "resolve": {"q_rerank": run.last["q_rerank"], "q_full": run.last["q_full"]} if run.last else None,
             "empty_repairs_on_device": run.device_repairs,
-            "arith": "fp16x3 MFMA screen with a rigorous bound, float64 exact re-rank of ambiguous points, "
-                     "float64 partial sums",
+            "screen": screen,
+            "arith": ("fp16 MFMA screen (balanced image, pairwise bound)" if screen in (2, 3) else
+                      "fp16x3 MFMA screen with a rigorous bound") +
+                     ", float64 exact re-rank of ambiguous points, float64 partial sums",
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(d, k, N, args.cpu_seconds)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KM_ABI_VERSION 2
+#define KM_ABI_VERSION 3
 
 #define KM_OK 0
 #define KM_EMPTY 1          /* informational: the update found empty clusters */
@@ -195,6 +195,17 @@ int km_bernoulli_sample(km_ctx* ctx, const uint64_t* seeds, const int64_t* sizes
 int km_predict(km_ctx* ctx, int32_t* labels_out);
 /* Labels of the last km_assign_stats (device -> host). */
 int km_labels(km_ctx* ctx, int32_t* labels_out);
+
+/* Screening kernel of the fused path (k = 256, d <= 64 class).  A cost
+ * choice: labels, sums and SSE are exact in every mode.  -1 (default): per
+ * batch from the last iteration's queue fraction; 0: fp16x3 screen, global
+ * bound; 1: fp16x3 with per-key bounds; 2: fast screen (one fp16 MFMA per
+ * product, pairwise bound); 3: fast screen with the row split hi + lo.
+ * Modes 2 and 3 fall back to 0 where the fast kernel has no instance. */
+#define KM_SCREEN_AUTO (-1)
+int km_set_screen(km_ctx* ctx, int32_t mode);
+/* The screen the next fused launch uses (0..3). */
+int km_get_screen(km_ctx* ctx, int32_t* mode);
 
 /* Kernel timing with HIP events on the context stream.  `enable` is a
  * bitmask of (1 << KM_K_*) phases to time (-1: all, 0: off). */
