@@ -305,15 +305,20 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
         if (j < k) top3_insert(k1, k2, k3, key_of(acc, (uint32_t)j, mask));
       }
     } else {
+      // packed fp32 (v_pk_add_f32 / v_pk_fma_f32): even and odd features in
+      // two partial sums, half the VALU issue of the scalar loop; the
+      // direct-form bound (DP sequential terms) covers two sums of DP / 2
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
       for (int j = 0; j < k; ++j) {
-        const float* c = sC + j * DP;
-        float acc = 0.0f;
+        const f32x2* c2 = reinterpret_cast<const f32x2*>(sC + j * DP);
+        f32x2 acc2 = {0.0f, 0.0f};
 #pragma unroll
-        for (int f = 0; f < DP; ++f) {
-          const float t = x[f] - c[f];
-          acc = fmaf(t, t, acc);
+        for (int f = 0; f < DP; f += 2) {
+          const f32x2 xv = {x[f], x[f + 1]};
+          const f32x2 t = xv - c2[f / 2];
+          acc2 = __builtin_elementwise_fma(t, t, acc2);
         }
-        top3_insert(k1, k2, k3, key_of(acc, (uint32_t)j, mask));
+        top3_insert(k1, k2, k3, key_of(acc2.x + acc2.y, (uint32_t)j, mask));
       }
     }
     int lab = (int)(__float_as_uint(k1) & mask);
