@@ -1666,6 +1666,7 @@ __device__ __forceinline__ _Float16 f16_step(_Float16 h, bool up) {
 // bal[1] = max_j |alpha_j . c'_j| (scaled units, rounded up; real centroids).
 __global__ __launch_bounds__(512) void k_prep_bal(const float* __restrict__ C32, int k, int kp, int dp,
                                                   const float* __restrict__ xabs, const float* __restrict__ cabs,
+                                                  const float* __restrict__ cmaxp, int nx,
                                                   uint16_t* __restrict__ imgF, float* __restrict__ bal,
                                                   const int* __restrict__ gate) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
@@ -1739,8 +1740,35 @@ __global__ __launch_bounds__(512) void k_prep_bal(const float* __restrict__ C32,
       m0 = fmaxf(m0, red[0][w]);
       m1 = fmaxf(m1, red[1][w]);
     }
-    bal[0] = m0;
-    bal[1] = m1;
+    // pairwise-bound constants (scaled units), every per-point term affine
+    // in xn = s ||x|| (per-row upper bound): bal[2..10] = s, cm, G1, G0, c1,
+    // c0, h1, h0, rho2 (k_fused1 reads them as scalars)
+    const float cm = *cmaxp * s;
+    const float pm = (*cabs * s) * (*xabs * s) * 1.0001f;
+    const float sq = sqrtf((float)dp);
+    // fp16 subnormals (flushed or not): 2^-14 per element, on row and image
+    // (|alpha_f| grows by <= 2^-14 only where |c'_f| < 2^-15)
+    const float an = m0 + 6.103515625e-05f * sq, ac = m1 + (float)dp * 1.862645149230957e-09f;
+    const float NM = (float)(nx * dp / 16);  // MFMAs per score chain
+    // ||beta|| <= bq1 xn + bq0 (row rounding: u16 = 2^-11; hi + lo: u16^2)
+    const float bq1 = (nx == 1 ? 4.8828125e-4f : 2.384185791015625e-07f) * 1.0001f;
+    const float bq0 = 6.103515625e-05f * sq;
+    // accumulation (one rounding of |D| <= cm^2 + 2 cm xn per MFMA, and the
+    // in-group alignment truncation, 14 u24 x the largest product 2 pm)
+    const float acc1 = NM * U24 * 2.01f * cm;
+    const float acc0 = NM * U24 * (cm * cm + 28.1f * pm);
+    const float nu = 1.01f * U24 * cm * cm;  // ||c||^2 s^2 rounding
+    // |E_j| <= G = Acc + nu + 2 u24 cm xn + 2 cm ||beta|| + max||alpha|| (xn + ||beta||)
+    bal[2] = s;
+    bal[3] = cm;
+    bal[4] = acc1 + 2.01f * U24 * cm + 2.01f * cm * bq1 + an * (1.0f + bq1);
+    bal[5] = acc0 + nu + 2.01f * cm * bq0 + an * bq0;
+    bal[6] = 2.0f * bq1;
+    bal[7] = 2.0f * bq0 + an * 1.0001f;
+    bal[8] = 2.0f * acc1 + 4.01f * U24 * cm + 2.0f * an * bq1;
+    bal[9] = 2.0f * acc0 + 2.0f * nu + 2.0f * ac + 2.0f * an * bq0;
+    // key truncation (index bits of kp) plus the rounding of a key difference
+    bal[10] = __builtin_ldexpf(1.0f, ceil_log2(kp) - 2 - 23) * 1.01f + 2.0f * U24;
   }
 }
 
@@ -1780,32 +1808,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_fused1(FusedArgs A, const flo
     for (int t = 0; t < NS; ++t) asm volatile("" : "+a"(Ahi[b][t]));
   __syncthreads();
 
-  const float s = mfma_scale(*A.xabs, *A.cabs);
-  // pairwise-bound constants (scaled units), every per-point term affine in
-  // xn = s ||x|| (per-row upper bound)
-  const float cm = *cmaxp * s;
-  const float pm = (*A.cabs * s) * (*A.xabs * s) * 1.0001f;
-  const float sq = sqrtf((float)DP);
-  // fp16 subnormals (flushed or not): 2^-14 per element, on row and image
-  // (|alpha_f| grows by <= 2^-14 only where |c'_f| < 2^-15)
-  const float an = bal[0] + 6.103515625e-05f * sq, ac = bal[1] + (float)DP * 1.862645149230957e-09f;
-  constexpr float NM = (float)(NX * NS);  // MFMAs per score chain
-  // ||beta|| <= bq1 xn + bq0 (row rounding: u16 = 2^-11; hi + lo: u16^2)
-  const float bq1 = (NX == 1 ? 4.8828125e-4f : 2.384185791015625e-07f) * 1.0001f;
-  const float bq0 = 6.103515625e-05f * sq;
-  // accumulation (one rounding of |D| <= cm^2 + 2 cm xn per MFMA, and the
-  // in-group alignment truncation, 14 u24 x the largest product 2 pm)
-  const float acc1 = NM * U24 * 2.01f * cm;
-  const float acc0 = NM * U24 * (cm * cm + 28.1f * pm);
-  const float nu = 1.01f * U24 * cm * cm;  // ||c||^2 s^2 rounding
-  // |E_j| <= G = Acc + nu + 2 u24 cm xn + 2 cm ||beta|| + max||alpha|| (xn + ||beta||)
-  const float G1 = acc1 + 2.01f * U24 * cm + 2.01f * cm * bq1 + an * (1.0f + bq1);
-  const float G0 = acc0 + nu + 2.01f * cm * bq0 + an * bq0;
-  const float c1 = 2.0f * bq1, c0 = 2.0f * bq0 + an * 1.0001f;
-  const float h1 = 2.0f * acc1 + 4.01f * U24 * cm + 2.0f * an * bq1;
-  const float h0 = 2.0f * acc0 + 2.0f * nu + 2.0f * ac + 2.0f * an * bq0;
-  // key truncation (index bits) plus the rounding of a key difference
-  const float rho2 = __builtin_ldexpf(1.0f, B - 2 - 23) * 1.01f + 2.0f * U24;
+  // pairwise-bound constants from k_prep_bal (uniform: scalar loads)
+  const float s = bal[2], cm = bal[3];
+  const float G1 = bal[4], G0 = bal[5], c1 = bal[6], c0 = bal[7], h1 = bal[8], h0 = bal[9];
+  const float rho2 = bal[10];
 
   const int64_t n = A.n;
   const int64_t ntiles = (n + 31) / 32;
@@ -2017,16 +2023,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_fused1(FusedArgs A, const flo
     }
   };
 
-  float4 xb0[NS][2], xb1[NS][2];
-  float xn0 = 0.0f, xn1 = 0.0f;
-  load_tile(gw, xb0, xn0);
-  for (int64_t tile = gw; tile < ntiles; tile += 2 * tstride) {
-    const int64_t t1 = tile + tstride;
-    load_tile(t1, xb1, xn1);
-    process_tile(tile, xb0, xn0);
-    if (t1 >= ntiles) break;
-    load_tile(t1 + tstride, xb0, xn0);
-    process_tile(t1, xb1, xn1);
+  {
+    float4 xb0[NS][2], xb1[NS][2];
+    float xn0 = 0.0f, xn1 = 0.0f;
+    load_tile(gw, xb0, xn0);
+    for (int64_t tile = gw; tile < ntiles; tile += 2 * tstride) {
+      const int64_t t1 = tile + tstride;
+      load_tile(t1, xb1, xn1);
+      process_tile(tile, xb0, xn0);
+      if (t1 >= ntiles) break;
+      load_tile(t1 + tstride, xb0, xn0);
+      process_tile(t1, xb1, xn1);
+    }
   }
   if (lane == 0) {
     A.qcount[2 * gw] = qn;
@@ -2160,8 +2168,8 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
   const int ns = g.dp / 16, nb = g.kp / 32;
   const int refine = (mode == KM_SCREEN_X3_REFINE) ? 1 : 0;
   if ((mode == KM_SCREEN_FAST1 || mode == KM_SCREEN_FAST2) && fast_path_ok(g)) {
-    hipLaunchKernelGGL(k_prep_bal, dim3(1), dim3(512), 0, s, C32, g.k, g.kp, g.dp, xabs, cabs,
-                       reinterpret_cast<uint16_t*>(ChiF), bal, gate);
+    hipLaunchKernelGGL(k_prep_bal, dim3(1), dim3(512), 0, s, C32, g.k, g.kp, g.dp, xabs, cabs, cmax,
+                       mode == KM_SCREEN_FAST1 ? 1 : 2, reinterpret_cast<uint16_t*>(ChiF), bal, gate);
     constexpr int WAVES = 4;
     const int64_t ntiles = (g.n + 31) / 32;
     int64_t blocks = n_cu;

@@ -620,8 +620,8 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
     KM_HIP(hipMalloc(&c->cn2s, sizeof(float) * kp));
     KM_HIP(hipMalloc(&c->ChiF, sizeof(_Float16) * kp * dp));
     KM_HIP(hipMalloc(&c->CloF, sizeof(_Float16) * kp * dp));
-    KM_HIP(hipMalloc(&c->bnd, sizeof(float) * 4));
-    c->bal = c->bnd + 2;  // [0, 1]: screening-bound constants, [2, 3]: fast screen image maxima
+    KM_HIP(hipMalloc(&c->bnd, sizeof(float) * 16));
+    c->bal = c->bnd + 4;  // [0, 1]: screening-bound constants; bal[0..10]: fast screen image maxima and bound constants
     KM_HIP(hipMalloc(&c->cmax, sizeof(float)));
     KM_HIP(hipMalloc(&c->cabs, sizeof(float)));
     KM_HIP(hipMalloc(&c->stats_own, sizeof(double) * stats_len(c->g)));

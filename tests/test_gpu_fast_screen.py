@@ -179,7 +179,13 @@ def test_auto_policy_switches_to_fast_screen_and_stays_exact():
     km.verbose = False
     km.fit(X)
     assert km._runner.engine.screen() == 2
-    ref = orc.lloyd_fit(X, 256, 40, 0.0, 0, True, 1, init_centroids=C0)
+    # the oracle validates tolerance > 0 like the reference: at 1e-300 it stops
+    # at the exact fixed point (shift 0), where the product keeps iterating
+    # on unchanged centroids
+    ref = orc.lloyd_fit(X, 256, 40, 1e-300, 0, True, 1, init_centroids=C0)
+    m = len(ref["sse_history"])
+    assert len(km.sse_history) == 40 and m <= 40
     np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
-    np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)
+    np.testing.assert_allclose(km.sse_history[:m], ref["sse_history"], rtol=1e-9)
+    np.testing.assert_allclose(km.sse_history[m:], [ref["sse_history"][-1]] * (40 - m), rtol=1e-9)
     np.testing.assert_array_equal(km.predict(X).to_numpy(), orc.assign(X, ref["centroids"])[0])
