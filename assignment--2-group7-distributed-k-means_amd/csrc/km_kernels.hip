@@ -539,6 +539,9 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int KC = A.KC;
   const size_t himg = (size_t)(KC / 32) * BLKB;
+  // one chunk image: hi, lo, ||c||^2 s^2; with several chunks two of them
+  // (double buffer, filled by LDS-DMA while the other is read)
+  const size_t bufsz = ((2 * himg + (size_t)KC * 4) + 15) / 16 * 16;
   char* sHi = smem;
   char* sLo = smem + himg;
   float* sCn = reinterpret_cast<float*>(smem + 2 * himg);
@@ -575,9 +578,40 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
     for (int id = threadIdx.x; id < kc; id += WAVES * 64) sCn[id] = A.cn2s[(size_t)ch * KC + id];
   };
 
+  // several chunks: chunk images through LDS-DMA (global_load_lds, 16 B per
+  // lane, no VGPRs), one 1 KiB fragment piece per wave-instruction, into the
+  // buffer the waves are not reading; the barrier at each chunk start drains
+  // the wave's own DMA (vmcnt) and then everyone's
+  auto stage_async = [&](int ch, int bf) {
+    const int kc = min(KC, kp - ch * KC);
+    const int npc = (kc / 32) * NS;  // 1 KiB pieces per image
+    char* dHi = smem + (size_t)bf * bufsz;
+    char* dLo = dHi + himg;
+    char* dCn = dHi + 2 * himg;
+    const char* gh = reinterpret_cast<const char*>(A.Chi + (size_t)ch * KC * DP);
+    const char* gl = reinterpret_cast<const char*>(A.Clo + (size_t)ch * KC * DP);
+    for (int pc = wave; pc < npc; pc += WAVES) {
+      const int blk = pc / NS, t = pc - blk * NS;
+      const size_t src = ((size_t)(blk * 32 + r) * DP + 16 * t + 8 * h) * 2;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(gh + src),
+                                       (__attribute__((address_space(3))) void*)(dHi + (size_t)pc * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(gl + src),
+                                       (__attribute__((address_space(3))) void*)(dLo + (size_t)pc * 1024), 16, 0, 0);
+    }
+    // ||c||^2 s^2 of the chunk: kc * 4 bytes, 1 KiB per wave-instruction
+    const char* gc = reinterpret_cast<const char*>(A.cn2s + (size_t)ch * KC);
+    for (int pc = wave; pc * 1024 < kc * 4; pc += WAVES)
+      if (pc * 1024 + lane * 16 < kc * 4)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(gc + pc * 1024 + lane * 16),
+                                         (__attribute__((address_space(3))) void*)(dCn + pc * 1024), 16, 0, 0);
+  };
+
+  int cbuf = 0;  // buffer the current chunk is in (several chunks)
   if (nchunks == 1) {
     stage(0);
     __syncthreads();
+  } else if ((int64_t)blockIdx.x < nwt) {
+    stage_async(0, 0);
   }
 
   // per-wave queue segment: no global counter (one hot address would
@@ -588,6 +622,11 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
   const char* laneHi = sHi + lane * 16;
   const char* laneLo = sLo + lane * 16;
   const float* laneCn = sCn + 4 * h;
+  auto point_at = [&](int bf) {
+    laneHi = smem + (size_t)bf * bufsz + lane * 16;
+    laneLo = laneHi + himg;
+    laneCn = reinterpret_cast<const float*>(smem + (size_t)bf * bufsz + 2 * himg) + 4 * h;
+  };
 
   for (int64_t wt = blockIdx.x; wt < nwt; wt += gridDim.x) {
     const int64_t tile = wt * WAVES + wave;
@@ -713,9 +752,13 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
 
     for (int ch = 0; ch < nchunks; ++ch) {
       if (nchunks > 1) {
-        __syncthreads();
-        stage(ch);
-        __syncthreads();
+        __syncthreads();  // this chunk's DMA landed; the other buffer is no longer read
+        point_at(cbuf);
+        if (ch + 1 < nchunks)
+          stage_async(ch + 1, cbuf ^ 1);
+        else if (wt + gridDim.x < nwt)
+          stage_async(0, cbuf ^ 1);  // the next tile group starts over at chunk 0
+        cbuf ^= 1;
         fr = load_frag(0, 0);
       }
       const int nb = min(KC, kp - ch * KC) / 32;  // even: kp and KC are multiples of 64
@@ -1040,7 +1083,7 @@ static int mfma_kc(const Geometry& g, int* waves) {
   const size_t per = (size_t)g.dp * 4 + 4;
   *waves = (g.dp >= 192) ? 4 : (g.dp <= 64 ? mfma_waves_env() : 8);
   if ((size_t)g.kp * per <= MFMA_LDS_LARGE) return g.kp;
-  return (int)((MFMA_LDS_LARGE / per) / 64 * 64);
+  return (int)((MFMA_LDS_LARGE / 2 / per) / 64 * 64);  // two chunk buffers
 }
 
 // at most 2 workgroups x 8 waves per CU, each wave's segment rounded up to
@@ -1126,7 +1169,8 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
   int waves = 8;
   const int KC = mfma_kc(g, &waves);
   if (KC < 64) return hipErrorInvalidValue;
-  const size_t lds = 2 * (size_t)KC * g.dp * 2 + (size_t)KC * 4;
+  const size_t bufsz = (2 * (size_t)KC * g.dp * 2 + (size_t)KC * 4 + 15) / 16 * 16;
+  const size_t lds = (KC < g.kp) ? 2 * bufsz : 2 * (size_t)KC * g.dp * 2 + (size_t)KC * 4;
   const int64_t ntiles = (g.n + 31) / 32;
   const int64_t nwt = (ntiles + waves - 1) / waves;
   int per_cu = (int)(MFMA_LDS_LARGE / lds);
