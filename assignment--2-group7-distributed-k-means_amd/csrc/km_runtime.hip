@@ -162,7 +162,16 @@ struct km_ctx {
   // profiling
   int prof = 0;                  // bitmask of KM_K_* phases timed with events
   const double* prep_of = nullptr;  // the centroid buffer the derived images were built from
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[KM_K_COUNT];
+  // timed launches: events, and the batch / slot of the iteration that
+  // enqueued them (a stopped batch's later launches are no-ops: km_batch_end
+  // drops their timings, so averages count launches that ran)
+  struct Timed {
+    hipEvent_t first, second;
+    int64_t batch;
+    int slot;
+  };
+  std::vector<Timed> ev[KM_K_COUNT];
+  int64_t batch_seq = 0;
   std::vector<hipEvent_t> pool;
 
   hipEvent_t take_event() {
@@ -193,7 +202,7 @@ struct ProfScope {
   ~ProfScope() {
     if ((c->prof >> kind) & 1) {
       (void)hipEventRecord(b, c->stream);
-      c->ev[kind].emplace_back(a, b);
+      c->ev[kind].push_back({a, b, c->in_batch ? c->batch_seq : -1, c->batch_n});
     }
   }
 };
@@ -782,6 +791,7 @@ int km_batch_begin(km_ctx* c) {
   KM_HIP(hipMemsetAsync(c->gate, 0, sizeof(int), c->stream));
   c->in_batch = true;
   c->batch_n = 0;
+  ++c->batch_seq;
   return KM_OK;
 }
 
@@ -846,6 +856,18 @@ int km_batch_end(km_ctx* c, km_status* st, int64_t* counts, int32_t* n_ran) {
   int ran = 0;
   while (ran < m && c->hist_host[ran].ran) ++ran;
   *n_ran = ran;
+  for (auto& v : c->ev) {
+    size_t w = 0;
+    for (size_t i = 0; i < v.size(); ++i) {
+      if (v[i].batch == c->batch_seq && v[i].slot >= ran) {  // a no-op launch of the stopped batch
+        c->pool.push_back(v[i].first);
+        c->pool.push_back(v[i].second);
+      } else {
+        v[w++] = v[i];
+      }
+    }
+    v.resize(w);
+  }
   if (ran > 0) {
     // the state after the last iteration that ran, before its commit (as
     // after km_update): its old / new buffers, the new one's images prepared
