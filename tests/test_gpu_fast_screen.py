@@ -189,3 +189,13 @@ def test_auto_policy_switches_to_fast_screen_and_stays_exact():
     np.testing.assert_allclose(km.sse_history[:m], ref["sse_history"], rtol=1e-9)
     np.testing.assert_allclose(km.sse_history[m:], [ref["sse_history"][-1]] * (40 - m), rtol=1e-9)
     np.testing.assert_array_equal(km.predict(X).to_numpy(), orc.assign(X, ref["centroids"])[0])
+
+
+@pytest.mark.parametrize("mode", [2, 3])
+@pytest.mark.parametrize("n,d,k", [(20000, 32, 128), (9000, 48, 200)])
+def test_fast_modes_fall_back_outside_the_fast_shape(mode, n, d, k):
+    # the fast kernel exists for dp = 64, kp = 256 only; elsewhere a forced
+    # fast mode runs the fp16x3 fused kernel (km_set_screen): same results
+    X = _blobs(n, d, k // 2, seed=d + k)
+    C0 = X[np.random.default_rng(4).choice(n, k, replace=False)]
+    _check(X, C0, mode)
