@@ -465,3 +465,11 @@ def test_take_sample_split_over_ranks_is_identical():
         assert p.exitcode == 0
     for _, a, b in res:
         assert (a, b) == want
+
+
+def test_graft_build_entry_matches_the_library_abi():
+    # __graft_entry__.build() (the driver's build check) runs make (a no-op when
+    # the library is current) and checks the loaded library's ABI version
+    # against the package constant; a stale pin here once broke it
+    import __graft_entry__ as g
+    g.build()
