@@ -84,7 +84,7 @@ bool mfma_path_ok(const Geometry& g);
 // stats != nullptr: also add the resolved points' rows to the partial sums
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
-                          double* stats, int n_cu, const int* gate, hipStream_t s);
+                          double* stats, int n_cu, const int* gate, hipStream_t s, double* sse = nullptr);
 // Fused assign + partial sums (kp*dp <= 16384 class): fp16 hi image in VGPRs,
 // lo image + float64 sum table in LDS; decided points summed here, queued
 // points (and their counts) by launch_resolve(stats).
@@ -110,7 +110,8 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
                         const _Float16* Clo, uint4* ChiF, uint4* CloF, const float* cn2s, const float* bnd,
                         const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,
                         double* stats, int with_stats, int mode, int n_cu, QLayout* ql, const int* gate,
-                        hipStream_t s, const float* C32, const float* cmax, float* bal);
+                        hipStream_t s, const float* C32, const float* cmax, float* bal, const double* C64P,
+                        double* sse);
 hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float* cabs, int dp, float* bnd,
                                const int* gate, hipStream_t s);
 hipError_t launch_row_norm(const float* X, const Geometry& g, float* xnorm, hipStream_t s);
@@ -121,12 +122,9 @@ size_t sorted_stats_words(int64_t n, int k);
 // C64P != nullptr: the SSE residuals are accumulated in the same pass
 hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t* labels, double* stats,
                                uint32_t* scratch, const double* C64P, int n_cu, const int* gate, hipStream_t s);
+// C64P != nullptr: the SSE residuals are accumulated in the same pass
 hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels, double* stats, int n_cu,
-                        const int* gate, hipStream_t s);
-// SSE of the final labels (kmeans_spark.py:224-237): sum over rows of the
-// float64 residual ||x - c_label||^2, added to *sse (one atomic per wave)
-hipError_t launch_sse(const float* X, const Geometry& g, const int32_t* labels, const double* C64P, double* sse,
-                      const int* gate, hipStream_t s);
+                        const int* gate, hipStream_t s, const double* C64P = nullptr);
 // stats = [k][d+1] sums and counts, then the SSE slot stats[k (d+1)]
 // gate: the batch's stop flag (kernels of later iterations no-op once it is
 // set); stop_tol >= 0 lets k_finalize raise it (KM_STOP_*), < 0 never

@@ -752,7 +752,12 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
 
     for (int ch = 0; ch < nchunks; ++ch) {
       if (nchunks > 1) {
-        __syncthreads();  // this chunk's DMA landed; the other buffer is no longer read
+        // this chunk's DMA landed: LDS-DMA completion is tracked only by the
+        // issuing wave's vmcnt, and a workgroup barrier on gfx950 does not
+        // drain it (the compiler inserts no vmcnt wait before s_barrier), so
+        // every wave waits for its own pieces first, then for everyone's
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // ... and the other buffer is no longer read
         point_at(cbuf);
         if (ch + 1 < nchunks)
           stage_async(ch + 1, cbuf ^ 1);
@@ -1282,6 +1287,8 @@ struct FusedArgs {
   uint32_t* qcount;
   double* stats;       // [k][d+1] (sums, counts)
   const int* gate;     // nonzero: a stopped batch, the launch is a no-op
+  const double* C64P;  // SSE variant: float64 centroids padded [kp][dp] (L2-resident)
+  double* sse;         // SSE variant: the SSE slot stats[k (d+1)]
 };
 
 constexpr int ceil_log2_c(int v) { return v <= 1 ? 0 : 1 + ceil_log2_c((v + 1) / 2); }
@@ -1297,7 +1304,10 @@ __device__ __forceinline__ void perm_halves(uint32_t v, uint32_t& lo, uint32_t& 
 // 1 = no key updates, 2 = no MFMAs, 3 = no LDS sums, 4 = no merge / queue,
 // 5 = MFMAs + conversion + loads only, 6 = as 5 with L2-resident rows,
 // 7 = full kernel with s_memtime phase stamps, 8 = full kernel, compiler schedule
-template <int NS, int NB, bool STATS, int ABL = 0, bool REF = true>
+// SSE (compute_sse, kmeans_spark.py:224-237): every decided row's float64
+// residual to its pre-update centroid (C64P, gathered from L2 by label) is
+// summed in the same pass; queued rows get theirs from the resolvers
+template <int NS, int NB, bool STATS, int ABL = 0, bool REF = true, bool SSE = false>
 __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   constexpr int DP = 16 * NS;
@@ -1363,6 +1373,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   unsigned long long st_acc[5] = {0, 0, 0, 0, 0};
   unsigned long long st_last = 0;
   if constexpr (ABL == 7) st_last = __builtin_amdgcn_s_memtime();
+  double ss_acc = 0.0;  // SSE variant: this lane's residual sum
   auto process_tile = [&](int64_t tile, const float4 (&xc)[NS][2], float xn) {
     const int64_t row = tile * 32 + r;
     const bool valid = row < n;
@@ -1629,6 +1640,29 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
           for (int e = 0; e < 8; ++e) atomicAdd(tp + (size_t)(16 * t + e) * TS, (double)xe[e]);
         }
         if (h == 0) atomicAdd(tab + (size_t)DP * TS + lab, 1.0);  // count row
+        if constexpr (SSE) {
+          // this lane's 8 NS features of the row against the float64
+          // centroid (padded features are 0 - 0)
+          const double* cr = A.C64P + (size_t)lab * DP + 8 * h;
+#pragma unroll
+          for (int t = 0; t < NS; ++t) {
+            const double4 ca = *reinterpret_cast<const double4*>(cr + 16 * t);
+            const double4 cb = *reinterpret_cast<const double4*>(cr + 16 * t + 4);
+            const float4 v0 = xc[t][0], v1 = xc[t][1];
+            const double r0 = (double)v0.x - ca.x, r1 = (double)v0.y - ca.y;
+            const double r2 = (double)v0.z - ca.z, r3 = (double)v0.w - ca.w;
+            const double r4 = (double)v1.x - cb.x, r5 = (double)v1.y - cb.y;
+            const double r6 = (double)v1.z - cb.z, r7 = (double)v1.w - cb.w;
+            ss_acc = fma(r0, r0, ss_acc);
+            ss_acc = fma(r1, r1, ss_acc);
+            ss_acc = fma(r2, r2, ss_acc);
+            ss_acc = fma(r3, r3, ss_acc);
+            ss_acc = fma(r4, r4, ss_acc);
+            ss_acc = fma(r5, r5, ss_acc);
+            ss_acc = fma(r6, r6, ss_acc);
+            ss_acc = fma(r7, r7, ss_acc);
+          }
+        }
       }
     }
     if constexpr (ABL == 7) {
@@ -1660,6 +1694,10 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
     A.qcount[2 * gw] = qn;
     A.qcount[2 * gw + 1] = qf;
   }
+  if constexpr (SSE) {
+    ss_acc = wave_sum(ss_acc);
+    if (lane == 0 && ss_acc != 0.0) atomicAdd(A.sse, ss_acc);
+  }
   if constexpr (ABL == 7) {
     if (lane == 0)
       for (int i = 0; i < 5; ++i) atomicAdd(&g_stamp[i], st_acc[i]);
@@ -1678,6 +1716,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   }
 }
 
+#ifdef KM_DIAG  // the fast screen is a diagnostic-build experiment (DESIGN.md "Fast screen")
 // ---------------------------------------------------------------------------
 // Fast screen (k_fused1): ONE fp16 image of -2cs (128 AGPRs instead of 256)
 // against the row as one fp16 part (NX = 1: one MFMA per product instead of
@@ -2096,6 +2135,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_fused1(FusedArgs A, const flo
   }
 }
 
+#endif  // KM_DIAG
+
 // fragment-linear copies of the hi / lo images: piece (b, t), lane l holds
 // 8 halves of row 32 b + (l & 31), features 16 t + 8 (l >> 5) .. + 8
 __global__ __launch_bounds__(256) void k_frag_images(const _Float16* __restrict__ Chi, const _Float16* __restrict__ Clo,
@@ -2205,13 +2246,15 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
                         const _Float16* Clo, uint4* ChiF, uint4* CloF, const float* cn2s, const float* bnd,
                         const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,
                         double* stats, int with_stats, int mode, int n_cu, QLayout* ql, const int* gate,
-                        hipStream_t s, const float* C32, const float* cmax, float* bal) {
+                        hipStream_t s, const float* C32, const float* cmax, float* bal, const double* C64P,
+                        double* sse) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
   const int ns = g.dp / 16, nb = g.kp / 32;
   const int refine = (mode == KM_SCREEN_X3_REFINE) ? 1 : 0;
-  if ((mode == KM_SCREEN_FAST1 || mode == KM_SCREEN_FAST2) && fast_path_ok(g)) {
+#ifdef KM_DIAG
+  if ((mode == KM_SCREEN_FAST1 || mode == KM_SCREEN_FAST2) && fast_path_ok(g) && !(with_stats && sse)) {
     hipLaunchKernelGGL(k_prep_bal, dim3(1), dim3(512), 0, s, C32, g.k, g.kp, g.dp, xabs, cabs, cmax,
                        mode == KM_SCREEN_FAST1 ? 1 : 2, reinterpret_cast<uint16_t*>(ChiF), bal, gate);
     constexpr int WAVES = 4;
@@ -2223,7 +2266,8 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
     const uint32_t seg = (uint32_t)(((ntiles + nw - 1) / nw) * 32);
     ql->seg = seg;
     ql->nwaves = (uint32_t)nw;
-    FusedArgs a{X, xnorm, g.n, g.k, g.d, seg, ChiF, CloF, cn2s, bnd, xabs, cabs, labels, queue, qcount, stats, gate};
+    FusedArgs a{X, xnorm, g.n, g.k, g.d, seg, ChiF, CloF, cn2s, bnd, xabs, cabs, labels, queue, qcount, stats, gate,
+                C64P, sse};
     const size_t lds = (size_t)g.kp * 4 + (with_stats ? (size_t)(g.dp + 1) * g.kp * 8 : 0);
     if (mode == KM_SCREEN_FAST1) {
       if (with_stats)
@@ -2238,6 +2282,7 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
     }
     return hipGetLastError();
   }
+#endif
   {
     const int total = nb * ns * 64;
     hipLaunchKernelGGL(k_frag_images, dim3((total + 255) / 256), dim3(256), 0, s, Chi, Clo, g.kp, g.dp, ChiF, CloF, gate);
@@ -2251,11 +2296,14 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
   const uint32_t seg = (uint32_t)(((ntiles + nw - 1) / nw) * 32);
   ql->seg = seg;
   ql->nwaves = (uint32_t)nw;
-  FusedArgs a{X, xnorm, g.n, g.k, g.d, seg, ChiF, CloF, cn2s, bnd, xabs, cabs, labels, queue, qcount, stats, gate};
+  FusedArgs a{X, xnorm, g.n, g.k, g.d, seg, ChiF, CloF, cn2s, bnd, xabs, cabs, labels, queue, qcount, stats, gate,
+                C64P, sse};
   const size_t lds = (size_t)g.kp * 4 + (with_stats ? (size_t)(g.dp + 1) * g.kp * 8 : 0);
 #define KM_FUSED_CASE(NS_, NB_)                                                                        \
   case NS_ * 100 + NB_:                                                                                \
-    if (with_stats && !refine)                                                                         \
+    if (with_stats && sse)                                                                             \
+      hipLaunchKernelGGL((k_fused<NS_, NB_, true, 0, true, true>), dim3(nbk), dim3(256), lds, s, a);   \
+    else if (with_stats && !refine)                                                                    \
       hipLaunchKernelGGL((k_fused<NS_, NB_, true, 0, false>), dim3(nbk), dim3(256), lds, s, a);        \
     else if (with_stats)                                                                               \
       hipLaunchKernelGGL((k_fused<NS_, NB_, true>), dim3(nbk), dim3(256), lds, s, a);                  \
@@ -2386,7 +2434,7 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
                                                   const double* __restrict__ C64, const QEntry* __restrict__ queue,
                                                   const uint32_t* __restrict__ qcount, QLayout ql,
                                                   int32_t* __restrict__ labels, double* __restrict__ stats,
-                                                  int tab_kp, const int* __restrict__ gate) {
+                                                  int tab_kp, double* __restrict__ sse, const int* __restrict__ gate) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* tab = reinterpret_cast<double*>(smem);
@@ -2399,6 +2447,7 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
   const uint32_t total = pre[ql.nwaves];
   const int u = threadIdx.x & 7;
   const uint32_t ng = (gridDim.x * blockDim.x) >> 3;
+  double ss_acc = 0.0;
   // the loop trip count is uniform over each 8-lane group (shuffles inside)
   for (uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 3; g < total + ((ng - total % ng) % ng);
        g += ng) {
@@ -2425,6 +2474,7 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
       np_pw8<2>(sq2, 0, d, u, sa, sb);
     int lab = np_pick_second(sqrt(sa), sqrt(sb)) ? bb : a;
     if (!have) continue;
+    double rsq_bad = 0.0;
     if (!ok && u == 0) {
       // corrupt candidate (cannot happen for finite data): full scan
       double best = 0.0;
@@ -2436,9 +2486,16 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
           lab = j;
         }
       }
+      rsq_bad = best;  // the norm (np_norm_d takes the sqrt)
     }
     if (!ok) lab = __shfl(lab, (int)(threadIdx.x & 63) & ~7);
     if (u == 0) labels[q.row] = lab;
+    // SSE (fused path): min_distance ** 2 with the chosen centroid's norm in
+    // NumPy's order (kmeans_spark.py:231-233)
+    if (sse && u == 0) {
+      const double mn = ok ? sqrt(lab == bb ? sb : sa) : rsq_bad;
+      ss_acc += mn * mn;
+    }
     if (stats) {
       for (int f = u; f < d; f += 8) {
         if (tab_kp)
@@ -2489,6 +2546,10 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
       if (v != 0.0 && j < k) atomicAdd(stats + (size_t)j * (d + 1) + f, v);
     }
   }
+  if (sse) {
+    ss_acc = wave_sum(ss_acc);  // lanes u == 0 hold the entries' terms
+    if ((threadIdx.x & 63) == 0 && ss_acc != 0.0) atomicAdd(sse, ss_acc);
+  }
 }
 
 // Full exact scans.  A workgroup (8 waves) takes batches of 8 G queued
@@ -2504,7 +2565,8 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
                                                    const double* __restrict__ C64T, const QEntry* __restrict__ queue,
                                                    const uint32_t* __restrict__ qcount, QLayout ql,
                                                    int32_t* __restrict__ labels, int ch,
-                                                   double* __restrict__ stats, int use_chain, int pair_chain, const int* __restrict__ gate) {
+                                                   double* __restrict__ stats, int use_chain, int pair_chain,
+                                                   double* __restrict__ sse, const int* __restrict__ gate) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sCT = reinterpret_cast<double*>(smem);                                    // [d][ch]
@@ -2516,6 +2578,7 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
   const int wave = threadIdx.x >> 6;
   float* xs = xs_all + (size_t)wave * G * d;
   const uint32_t per_batch = 8u * G;
+  double ss_acc = 0.0;  // SSE (fused path): lane 0's sum of the chosen sums of squares
   for (uint32_t b0 = blockIdx.x * per_batch; b0 < total; b0 += gridDim.x * per_batch) {
     uint32_t rows[G];
     bool have[G];
@@ -2574,6 +2637,7 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
       }
       const int lab = bi < 0 ? 0 : bi;
       if (lane == 0) labels[rows[g]] = lab;
+      if (sse && lane == 0 && bi >= 0) ss_acc += bv * bv;  // min_distance ** 2 (bv: the norm)
       if (stats) {
         for (int f = lane; f < d; f += 64) atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)xs[g * d + f]);
         if (lane == 0) atomicAdd(stats + (size_t)lab * (d + 1) + d, 1.0);  // count
@@ -2685,11 +2749,12 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
     for (int g = 0; g < G; ++g)
       if (have[g]) finish(g, best[g], bj[g]);
   }
+  if (sse && lane == 0 && ss_acc != 0.0) atomicAdd(sse, ss_acc);
 }
 
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
-                          double* stats, int n_cu, const int* gate, hipStream_t s) {
+                          double* stats, int n_cu, const int* gate, hipStream_t s, double* sse) {
   if (g.n == 0 || ql.nwaves == 0) return hipSuccess;
   constexpr size_t LDS_MAX = 160 * 1024;
   const size_t pre_bytes = ((size_t)ql.nwaves + 1) * 4;
@@ -2709,13 +2774,13 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   static const int fs_wg = diag_env("KM_FS_WG", 1);  // workgroups per CU (3: no measurable change)
   if (ch == 0)
     hipLaunchKernelGGL((k_fullscan<2, true>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
-                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, gate);
+                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, sse, gate);
   else if (G == 4)
     hipLaunchKernelGGL((k_fullscan<4, false>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
-                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, gate);
+                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, sse, gate);
   else
     hipLaunchKernelGGL((k_fullscan<2, false>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
-                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, gate);
+                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, sse, gate);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t tab_bytes = (size_t)(g.d + 1) * g.kp * 8;
@@ -2723,10 +2788,10 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   const int tab_kp = (stats && tab_bytes + pres <= LDS_MAX) ? g.kp : 0;
   if (g.d > 256)
     hipLaunchKernelGGL(k_rerank2<true>, dim3(n_cu), dim3(512), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
-                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, gate);
+                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate);
   else
     hipLaunchKernelGGL(k_rerank2<false>, dim3(n_cu), dim3(1024), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
-                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, gate);
+                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate);
   return hipGetLastError();
 }
 
@@ -2745,7 +2810,8 @@ static constexpr int STATS_LDS = 156 * 1024;
 // k (d+1) doubles exceed LDS but k (fr+1) fit (c4: 1024 clusters x 16 features).
 __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int64_t n, int d, int dp, int k,
                                                 const int32_t* __restrict__ labels, double* __restrict__ stats,
-                                                int kr, int fr, int64_t rows_per_block, const int* __restrict__ gate) {
+                                                int kr, int fr, int64_t rows_per_block, const double* __restrict__ C64P,
+                                                double* __restrict__ sse, const int* __restrict__ gate) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* tab = reinterpret_cast<double*>(smem);
@@ -2773,6 +2839,12 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
   // whole row idle (lane q = P would repeat row u + 1's first features)
   const bool act = q < P;
   constexpr int U = 8;         // float4 loads in flight per lane
+  // SSE (compute_sse, kmeans_spark.py:224-237) in the same pass: each
+  // (row, feature range) is summed by exactly one workgroup (the one owning
+  // the row's cluster), which adds the range's float64 residual to the
+  // row's pre-update centroid (C64P, L2-resident, gathered by label); the
+  // ranges' partial residuals sum to the row's
+  double ss = 0.0;
   for (int64_t cr = r0 + (int64_t)wave * 64; cr < r1; cr += (int64_t)nwaves * 64) {
     const int nrow = (int)min((int64_t)64, r1 - cr);
     const int labreg = lane < nrow ? labels[cr + lane] : -1;
@@ -2796,9 +2868,24 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
           atomicAdd(t + L, (double)v[u].y);
           atomicAdd(t + 2 * L, (double)v[u].z);
           atomicAdd(t + 3 * L, (double)v[u].w);
+          if (sse) {  // padded features are 0 - 0
+            const double* c = C64P + (size_t)lab * dp + f0 + 4 * mm;
+            const double2 ca = *reinterpret_cast<const double2*>(c);
+            const double2 cb = *reinterpret_cast<const double2*>(c + 2);
+            const double t0 = (double)v[u].x - ca.x, t1 = (double)v[u].y - ca.y;
+            const double t2 = (double)v[u].z - cb.x, t3 = (double)v[u].w - cb.y;
+            ss = fma(t0, t0, ss);
+            ss = fma(t1, t1, ss);
+            ss = fma(t2, t2, ss);
+            ss = fma(t3, t3, ss);
+          }
         }
       }
     }
+  }
+  if (sse) {
+    ss = wave_sum(ss);
+    if (lane == 0 && ss != 0.0) atomicAdd(sse, ss);
   }
   __syncthreads();
   const int d1 = d + 1;
@@ -2855,7 +2942,7 @@ static void stats_ranges(const Geometry& g, int* fr_out, int* kr_out) {
 }
 
 hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels, double* stats, int n_cu,
-                        const int* gate, hipStream_t s) {
+                        const int* gate, hipStream_t s, const double* C64P) {
   if (g.n == 0) return hipSuccess;
   if (g.dp > WIDE_MAX_DP || g.dp % 4) return hipErrorInvalidValue;
   int fr = 0, kr = 0;
@@ -2874,7 +2961,8 @@ hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels
   int64_t rpb = (g.n + bx - 1) / bx;
   rpb = (rpb + 63) / 64 * 64;
   hipLaunchKernelGGL(k_stats, dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024), lds, s, X, g.n,
-                     g.d, g.dp, g.k, labels, stats, kr, fr, rpb, gate);
+                     g.d, g.dp, g.k, labels, stats, kr, fr, rpb, C64P,
+                     C64P ? stats + (size_t)g.k * (g.d + 1) : (double*)nullptr, gate);
   return hipGetLastError();
 }
 
@@ -2886,6 +2974,45 @@ hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels
 // float64 by one workgroup with plain stores (no atomics): X is read once,
 // as gathered whole rows.
 // ---------------------------------------------------------------------------
+// Wave aggregation of label atomics.  Where a few clusters hold most rows (poor
+// seeds: c5_poor puts nearly all 50M rows in 3 clusters) one atomic per row
+// serialises every wave on the same few words.  The wave peels the label of
+// its first pending lane while that label is shared by at least two pending
+// lanes (at most PEEL rounds): the lowest such lane becomes the leader and
+// adds the group's size; every other lane adds 1 for itself.  All adds go out
+// as ONE atomic instruction (leaders and singles together).  Returns, per
+// lane, the count this lane adds (0: covered by its leader), the leader lane
+// and the lane's rank within its group (lanes in lane order).  Distinct labels
+// cost one ballot and stop the peeling at once.
+struct Peel {
+  uint32_t add;
+  int leader;
+  uint32_t rank;
+};
+template <int PEEL>
+__device__ __forceinline__ Peel peel_labels(int l, bool valid) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint64_t pending = __ballot(valid);
+  Peel p{0u, lane, 0u};
+#pragma unroll
+  for (int r = 0; r < PEEL; ++r) {
+    if (pending == 0ull) break;
+    const int first = __ffsll((unsigned long long)pending) - 1;
+    const int lead = __shfl(l, first);
+    const uint64_t mm = __ballot(valid && l == lead) & pending;
+    if (__popcll(mm) < 2) break;  // wave-uniform
+    if (lane == first) p.add = (uint32_t)__popcll(mm);
+    if ((mm >> lane) & 1ull) {
+      p.leader = first;
+      p.rank = (uint32_t)__popcll(mm & below);
+    }
+    pending &= ~mm;
+  }
+  if ((pending >> lane) & 1ull) p.add = 1u;  // a lane of its own
+  return p;
+}
+
 __global__ __launch_bounds__(1024) void k_hist(const int32_t* __restrict__ labels, int64_t n, int k,
                                                uint32_t* __restrict__ cnt, const int* __restrict__ gate) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
@@ -2893,9 +3020,14 @@ __global__ __launch_bounds__(1024) void k_hist(const int32_t* __restrict__ label
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
   for (int i = threadIdx.x; i < k; i += blockDim.x) hist[i] = 0u;
   __syncthreads();
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int l = labels[i];
-    if ((unsigned)l < (unsigned)k) atomicAdd(hist + l, 1u);
+  // wave-uniform trip count (every lane reaches the ballots of peel_labels)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < n; i0 += stride) {
+    const int64_t i = i0 + (threadIdx.x & 63);
+    const int l = i < n ? labels[i] : -1;
+    const bool valid = (unsigned)l < (unsigned)k;
+    const Peel p = peel_labels<4>(l, valid);
+    if (p.add) atomicAdd(hist + l, p.add);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < k; i += blockDim.x)
@@ -2936,10 +3068,19 @@ __global__ __launch_bounds__(256) void k_scatter(const int32_t* __restrict__ lab
                                                  uint32_t* __restrict__ cur, uint32_t* __restrict__ perm,
                                                  int32_t* __restrict__ slab, const int* __restrict__ gate) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int l = labels[i];
-    if ((unsigned)l < (unsigned)k) {
-      const uint32_t pos = atomicAdd(cur + l, 1u);
+  // one returning cursor atomic per (wave, hot label) instead of per row
+  // (peel_labels); wave-uniform trip count
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < n; i0 += stride) {
+    const int64_t i = i0 + (threadIdx.x & 63);
+    const int l = i < n ? labels[i] : -1;
+    const bool valid = (unsigned)l < (unsigned)k;
+    const Peel p = peel_labels<4>(l, valid);
+    uint32_t base = 0u;
+    if (p.add) base = atomicAdd(cur + l, p.add);
+    base = (uint32_t)__shfl((int)base, p.leader);
+    if (valid) {
+      const uint32_t pos = base + p.rank;
       perm[pos] = (uint32_t)i;
       slab[pos] = l;
     }
@@ -3037,113 +3178,6 @@ __global__ __launch_bounds__(256) void k_segsum(const float* __restrict__ X, int
     ss = wave_sum(ss);
     if (lane == 0 && ss != 0.0) atomicAdd(sse, ss);
   }
-}
-
-// SSE of the final labels (kmeans_spark.py:224-237) where no statistics pass
-// carries it: L = dp/4 lanes per row (float4 each), P = 64/L rows per
-// wave-instruction, U rows in flight per lane; the centroid features come
-// from the padded float64 copy (L2-resident) by label.
-template <int L>
-__global__ __launch_bounds__(256) void k_sse(const float* __restrict__ X, int64_t n,
-                                             const int32_t* __restrict__ labels, const double* __restrict__ C64P,
-                                             double* __restrict__ sse, const int* __restrict__ gate) {
-  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
-  constexpr int P = 64 / L;
-  constexpr int U = 4;
-  constexpr int DP = 4 * L;
-  const int lane = threadIdx.x & 63;
-  const int q = lane / L;
-  const int m = lane % L;
-  const bool act = q < P;
-  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  double ss = 0.0;
-  for (int64_t r0 = gw * (P * U); act && r0 < n; r0 += nw * (P * U)) {
-    float4 v[U];
-    int lb[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t row = r0 + u * P + q;
-      if (row < n) {
-        lb[u] = labels[row];
-        v[u] = *reinterpret_cast<const float4*>(X + (size_t)row * DP + 4 * m);
-      } else {
-        lb[u] = -1;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (lb[u] < 0) continue;
-      const double* c = C64P + (size_t)lb[u] * DP + 4 * m;
-      const double2 ca = *reinterpret_cast<const double2*>(c);
-      const double2 cb = *reinterpret_cast<const double2*>(c + 2);
-      const double t0 = (double)v[u].x - ca.x, t1 = (double)v[u].y - ca.y;
-      const double t2 = (double)v[u].z - cb.x, t3 = (double)v[u].w - cb.y;
-      ss = fma(t0, t0, ss);
-      ss = fma(t1, t1, ss);
-      ss = fma(t2, t2, ss);
-      ss = fma(t3, t3, ss);
-    }
-  }
-  ss = wave_sum(ss);
-  if (lane == 0 && ss != 0.0) atomicAdd(sse, ss);
-}
-
-// rows wider than 256 features: one row per wave, lanes over float4 slots
-__global__ __launch_bounds__(256) void k_sse_wide(const float* __restrict__ X, int64_t n, int dp,
-                                                  const int32_t* __restrict__ labels, const double* __restrict__ C64P,
-                                                  double* __restrict__ sse, const int* __restrict__ gate) {
-  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
-  const int lane = threadIdx.x & 63;
-  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  double ss = 0.0;
-  for (int64_t row = gw; row < n; row += nw) {
-    const int lb = labels[row];
-    const float* x = X + (size_t)row * dp;
-    const double* c = C64P + (size_t)lb * dp;
-    for (int f = 4 * lane; f < dp; f += 256) {
-      const float4 v = *reinterpret_cast<const float4*>(x + f);
-      const double2 ca = *reinterpret_cast<const double2*>(c + f);
-      const double2 cb = *reinterpret_cast<const double2*>(c + f + 2);
-      const double t0 = (double)v.x - ca.x, t1 = (double)v.y - ca.y;
-      const double t2 = (double)v.z - cb.x, t3 = (double)v.w - cb.y;
-      ss = fma(t0, t0, ss);
-      ss = fma(t1, t1, ss);
-      ss = fma(t2, t2, ss);
-      ss = fma(t3, t3, ss);
-    }
-  }
-  ss = wave_sum(ss);
-  if (lane == 0 && ss != 0.0) atomicAdd(sse, ss);
-}
-
-hipError_t launch_sse(const float* X, const Geometry& g, const int32_t* labels, const double* C64P, double* sse,
-                      const int* gate, hipStream_t s) {
-  if (g.n == 0) return hipSuccess;
-  if (g.dp > 256) {
-    int64_t blocks = (g.n + 3) / 4;
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(k_sse_wide, dim3((unsigned)blocks), dim3(256), 0, s, X, g.n, g.dp, labels, C64P, sse, gate);
-    return hipGetLastError();
-  }
-  const int L = g.dp / 4;
-  const int P = 64 / L;
-  int64_t blocks = (g.n + 4 * P * 4 - 1) / (4 * P * 4);  // 4 waves per block, P*4 rows per wave-step
-  if (blocks > 8192) blocks = 8192;
-  const dim3 grid((unsigned)blocks), blk(256);
-  switch (L) {
-    case 4: hipLaunchKernelGGL(k_sse<4>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
-    case 8: hipLaunchKernelGGL(k_sse<8>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
-    case 12: hipLaunchKernelGGL(k_sse<12>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
-    case 16: hipLaunchKernelGGL(k_sse<16>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
-    case 24: hipLaunchKernelGGL(k_sse<24>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
-    case 32: hipLaunchKernelGGL(k_sse<32>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
-    case 48: hipLaunchKernelGGL(k_sse<48>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
-    case 64: hipLaunchKernelGGL(k_sse<64>, grid, blk, 0, s, X, g.n, labels, C64P, sse, gate); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
 }
 
 // counts of the histogram into the count column

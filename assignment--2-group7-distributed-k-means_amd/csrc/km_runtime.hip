@@ -347,18 +347,16 @@ int run_assign(km_ctx* c, bool with_stats) {
       KM_HIP(km::launch_fused(c->X, c->xnorm, g, c->Chi, c->Clo, c->ChiF, c->CloF, c->cn2s, c->bnd, c->xabs, c->cabs,
                               c->labels, c->queue, c->qcount, c->stats, with_stats ? 1 : 0,
                               (with_stats || c->screen >= km::KM_SCREEN_FAST1) ? c->screen : km::KM_SCREEN_X3_REFINE,
-                              c->n_cu, &c->ql, c->gate, c->stream, c->C32, c->cmax, c->bal));
+                              c->n_cu, &c->ql, c->gate, c->stream, c->C32, c->cmax, c->bal, c->C64P,
+                              sse ? sse_slot : nullptr));
     }
     {
+      // SSE: the fused kernel adds every decided row's residual, the
+      // resolvers the queued rows' (same pass, no second read of X)
       ProfScope ps(c, KM_K_RESOLVE);
       KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels,
-                                with_stats ? c->stats : nullptr, c->n_cu, c->gate, c->stream));
-    }
-    if (sse) {
-      // the fused kernel's LDS holds the sum table: the residuals are a
-      // second pass over the final labels (only when compute_sse)
-      ProfScope ps(c, KM_K_STATS);
-      KM_HIP(km::launch_sse(c->X, g, c->labels, c->C64P, sse_slot, c->gate, c->stream));
+                                with_stats ? c->stats : nullptr, c->n_cu, c->gate, c->stream,
+                                sse ? sse_slot : nullptr));
     }
     return KM_OK;  // counts are part of the fused and resolver statistics
   }
@@ -384,8 +382,8 @@ int run_assign(km_ctx* c, bool with_stats) {
       KM_HIP(km::launch_stats_sorted(c->X, g, c->labels, c->stats, c->sort_scratch, sse ? c->C64P : nullptr,
                                      c->n_cu, c->gate, c->stream));
     } else {
-      KM_HIP(km::launch_stats(c->X, g, c->labels, c->stats, c->n_cu, c->gate, c->stream));
-      if (sse) KM_HIP(km::launch_sse(c->X, g, c->labels, c->C64P, sse_slot, c->gate, c->stream));
+      // SSE residuals in the same pass over X (feature-range tiles)
+      KM_HIP(km::launch_stats(c->X, g, c->labels, c->stats, c->n_cu, c->gate, c->stream, sse ? c->C64P : nullptr));
     }
   }
   return KM_OK;
@@ -586,6 +584,12 @@ int km_sum_x(km_ctx* c, double* out) {
 int km_set_screen(km_ctx* c, int32_t mode) {
   KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
   KM_REQUIRE(mode >= -1 && mode <= km::KM_SCREEN_FAST2, KM_ERR_ARG, "km_set_screen: mode must be -1..3");
+#ifndef KM_DIAG
+  // the fast screens (k_fused1) lost end to end on every BASELINE shape
+  // (DESIGN.md "Fast screen"): built in the diagnostic library only
+  KM_REQUIRE(mode <= km::KM_SCREEN_X3_REFINE, KM_ERR_UNSUPPORTED,
+             "km_set_screen: fast screens (modes 2, 3) are in the diagnostic build only");
+#endif
   c->screen_forced = mode;
   if (mode >= 0) c->screen = mode;
   return KM_OK;
@@ -697,8 +701,12 @@ int km_bind_stats_buffer(km_ctx* c, void* p) {
 }
 
 static int fast_mode() {
+#ifdef KM_DIAG
   static const int m = km::diag_env("KM_FAST", 1);  // diagnostic build: 0 off, 1 / 2 row parts
   return m == 0 ? -1 : (m == 2 ? km::KM_SCREEN_FAST2 : km::KM_SCREEN_FAST1);
+#else
+  return -1;  // product build: no fast screen
+#endif
 }
 
 static void note_queue(km_ctx* c, const km::DevStatus& s) {

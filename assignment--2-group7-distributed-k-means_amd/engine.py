@@ -100,8 +100,9 @@ class HipEngine:
 
     def set_screen(self, mode: int) -> None:
         """Screening kernel of the fused path (-1 auto; 0 fp16x3; 1 fp16x3 +
-        per-key bounds; 2 fast fp16 screen; 3 fast, row hi + lo).  A cost
-        choice only: results are exact in every mode (tests pin each one)."""
+        per-key bounds; 2 / 3 the fast fp16 screen, diagnostic library only).
+        A cost choice only: results are exact in every mode (tests pin each
+        one)."""
         self._c(self.lib.km_set_screen(self.ctx, int(mode)), "km_set_screen")
 
     def screen(self) -> int:

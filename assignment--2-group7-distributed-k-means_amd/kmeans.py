@@ -42,6 +42,7 @@ class LloydRunner:
         self.k = k
         self.last = None
         self.device_repairs = 0  # iterations whose empty clusters the device replaced
+        self.iterations_ran = 0  # iterations the device ran in batches (bench.py divides by these)
         # takeSample's Bernoulli pass on the GPU when the engine has one
         self.sampler = getattr(engine, "bernoulli", None)
 
@@ -88,12 +89,22 @@ class LloydRunner:
         while it < max_iter:
             m = min(size, max_iter - it)
             eng.batch_begin()
-            for _ in range(m):
-                eng.assign_stats()                             # L272 (+ L169-171 map side)
-                self.comm.allreduce_stats(eng)                 # L169-173 shuffle + collect
-                # L176-206 (+ the repair's seed int(time.time()), L196), device convergence test
-                eng.update_async(model.tolerance, model._empty_seed())
+            try:
+                for _ in range(m):
+                    eng.assign_stats()                         # L272 (+ L169-171 map side)
+                    self.comm.allreduce_stats(eng)             # L169-173 shuffle + collect
+                    # L176-206 (+ the repair's seed int(time.time()), L196), device convergence test
+                    eng.update_async(model.tolerance, model._empty_seed())
+            except BaseException:
+                # close the batch (the gate comes down, the context is back to
+                # the last iteration that ran), then report the original error
+                try:
+                    eng.batch_end(m)
+                except Exception:
+                    pass
+                raise
             recs = eng.batch_end(m)
+            self.iterations_ran += len(recs)
             # a batch that ran through doubles the next one (fewer host round
             # trips on long runs); a stopped one (convergence, empties) resets it
             size = min(2 * size, _lib.KM_MAX_BATCH) if len(recs) == m and not recs[-1][0].stop_reason else self.batch

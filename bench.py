@@ -43,6 +43,7 @@ CONFIGS = {
     "w784": (4_000_000, 784, 256, 256),
 }
 POOR_SEEDS = {"c5_poor"}
+SSE_CONFIGS = {"c4"}  # BASELINE.json configs[3]: "... compute_sse=True"
 HBM_PEAK_GBS = 8000.0                 # MI355X spec (MI355X_MICROARCH.md)
 F16_DENSE_TFLOPS = 2516.6             # dense f16/bf16 MFMA peak (MI355X_MICROARCH.md)
 F16X3_EFFECTIVE_TFLOPS = F16_DENSE_TFLOPS / 3.0  # fp16x3 split: 3 MFMAs per product
@@ -56,7 +57,11 @@ def parse():
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--screen", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
-                   help="fused-path screen (km_set_screen): -1 the runtime's per-batch choice")
+                   help="fused-path screen (km_set_screen): -1 the runtime's per-batch choice "
+                        "(2, 3: diagnostic library only)")
+    p.add_argument("--sse", type=int, default=None, choices=[0, 1],
+                   help="compute_sse (kmeans_spark.py:38); default: on for c4, whose BASELINE config "
+                        "(configs[3]) states compute_sse=True, off elsewhere (the reference default)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work per worker")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="per-launch HBM bytes from a rocprofv3 --pmc pass (optional)")
@@ -140,8 +145,9 @@ def main():
     from kmeans_amd.comm import Communicator
 
     N, d, k, centers = CONFIGS[args.config]
+    sse = bool(args.sse) if args.sse is not None else args.config in SSE_CONFIGS
     comm = Communicator()
-    km = kmeans_amd.KMeans(k=k, max_iter=10 ** 9, tolerance=1e-300, seed=42, compute_sse=False)
+    km = kmeans_amd.KMeans(k=k, max_iter=10 ** 9, tolerance=1e-300, seed=42, compute_sse=sse)
     km.verbose = False
     data = kmeans_amd.DeviceBlobs(n=N, d=d, n_centers=centers, box=10.0, std=1.0, seed=2024)
     run = km._make_runner(data, comm)
@@ -150,6 +156,7 @@ def main():
         C0 = np.vstack([C0[:3], np.full((k - 3, d), 100.0) + np.arange(k - 3)[:, None]])
     eng = run.engine
     eng.set_screen(args.screen)
+    eng.set_sse(sse)
     eng.set_centroids(C0)
     km.sse_history = []
 
@@ -167,12 +174,17 @@ def main():
     # record costs a few us of stream time); the other phases' durations come
     # from two untimed steps after it
     eng.profile(True, phases=("assign", "stats"))
+    ran0 = run.iterations_ran
     t0 = time.perf_counter()
     run.run(km, log, args.warmup + args.steps, first=args.warmup)
     eng.sync()
     torch.cuda.synchronize()
     comm.barrier()
     t1 = time.perf_counter()
+    # iterations the device actually ran in the timed region: a batch stops
+    # early only on convergence (max_shift < 1e-300, i.e. an exact fixed
+    # point), empties or NaN; the rate counts what ran, never args.steps
+    ran = run.iterations_ran - ran0
     eng.profile(True, phases=("resolve", "update", "prep"))
     run.run(km, log, args.warmup + args.steps + 2, first=args.warmup + args.steps)
     eng.sync()
@@ -243,13 +255,15 @@ def main():
     kernel_ms = {kk: (v[0] / max(v[1], 1)) for kk, v in kern.items()}
 
     if rank == 0:
-        it_s = args.steps / dt
+        it_s = ran / dt
         out = {
             "metric": METRIC, "value": it_s, "unit": "Lloyd it/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "steps_ran": ran, "warmup": args.warmup, "ms_per_step": dt / max(ran, 1) * 1e3,
+            "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic Gaussian blobs generated in HBM (centers U(-10,10), std 1)",
-            "config": {"workload": f"{args.config}: N={N} d={d} k={k}", "N": N, "d": d, "k": k,
+            "config": {"workload": f"{args.config}: N={N} d={d} k={k}" + (", compute_sse=True" if sse else ""),
+                       "N": N, "d": d, "k": k, "compute_sse": sse,
                        "parallelism": f"dp{world} (rows sharded, one RCCL all-reduce of k*(d+1) f64 per step)"},
             "points_per_sec": N * it_s, "roofline": roof, "kernel_avg_ms": kernel_ms,
             "resolve": {"q_rerank": run.last["q_rerank"], "q_full": run.last["q_full"]} if run.last else None,

@@ -112,7 +112,8 @@ int km_generate_blobs(km_ctx* ctx, int64_t n, int32_t d, int64_t global_row0, in
 int km_sum_x(km_ctx* ctx, double* out_d);
 /* compute_sse (kmeans_spark.py:38, 278-286): when enabled, km_assign_stats
  * also adds every row's float64 residual ||x - c_label||^2 to the SSE slot of
- * the stats buffer (replaces _compute_sse's second pass, :208-237). */
+ * the stats buffer, in the same pass over the rows that assigns them
+ * (replaces _compute_sse's second pass, :208-237). */
 int km_set_sse(km_ctx* ctx, int32_t enable);
 
 /* Set the current centroids: replaces sc.broadcast(self.centroids)
@@ -148,8 +149,9 @@ int km_update(km_ctx* ctx, km_status* st, int64_t* counts);
  * (PySpark's fraction, per-partition Bernoulli passes with CPython's MT19937,
  * retry, shuffle), its rows replace the empty clusters and their shifts enter
  * max_shift, without stopping the batch (km_status.repaired = 1).  Otherwise
- * (or if a pass overflows its slots or stays short twice) empty clusters stop
- * the batch and the caller repairs them. */
+ * (or if a pass overflows its slots or comes back short: the device does not
+ * retry PySpark's resampling loop) empty clusters stop the batch and the
+ * caller repairs them on the host with the same policy. */
 int km_set_layout(km_ctx* ctx, const int64_t* sizes, int32_t nparts, int64_t row0, int32_t device_repair);
 /* Batches of Lloyd iterations without host synchronisation (replaces the
  * per-iteration driver round trip of kmeans_spark.py:266-313).  Between
@@ -199,9 +201,10 @@ int km_labels(km_ctx* ctx, int32_t* labels_out);
 /* Screening kernel of the fused path (k = 256, d <= 64 class).  A cost
  * choice: labels, sums and SSE are exact in every mode.  -1 (default): per
  * batch from the last iteration's queue fraction; 0: fp16x3 screen, global
- * bound; 1: fp16x3 with per-key bounds; 2: fast screen (one fp16 MFMA per
- * product, pairwise bound); 3: fast screen with the row split hi + lo.
- * Modes 2 and 3 fall back to 0 where the fast kernel has no instance. */
+ * bound; 1: fp16x3 with per-key bounds.  Modes 2 and 3 (fast screen: one
+ * fp16 MFMA per product, pairwise bound; 3 with the row split hi + lo) exist
+ * in the diagnostic library only (libkmeans_amd_diag.so, make diag); the
+ * product library returns KM_ERR_UNSUPPORTED for them. */
 #define KM_SCREEN_AUTO (-1)
 int km_set_screen(km_ctx* ctx, int32_t mode);
 /* The screen the next fused launch uses (0..3). */

@@ -12,8 +12,18 @@ if GOLDEN not in sys.path:
     sys.path.insert(0, GOLDEN)
 
 
+# KM_LIB=diag: run against the diagnostic library (libkmeans_amd_diag.so,
+# `make -C <pkg>/csrc diag`), which adds the fast-screen experiment
+# (km_set_screen modes 2 and 3) to the product kernels
+DIAG_LIB = os.environ.get("KM_LIB") == "diag"
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+    if DIAG_LIB:
+        sys.path.insert(0, ROOT)
+        from kmeans_amd import _lib
+        _lib.LIB_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), "libkmeans_amd_diag.so")
 
 
 def load_golden(name):

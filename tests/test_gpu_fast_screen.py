@@ -1,11 +1,13 @@
 """Every screen of the fused kernel returns the reference's labels.
 
-The fused path (k_fused / k_fused1, the c3 class: k <= 256, d <= 64) has four
-screens (km_set_screen): fp16x3 with the global bound, fp16x3 with per-key
-bounds, and the fast screen (one fp16 MFMA per product against a balanced
-fp16 image, PAIRWISE bound; row as one fp16 part, or hi + lo).  The runtime
-picks one per batch from the queue fraction -- a cost choice, so each mode is
-forced here and held to the same bar as the automatic choice: labels equal to
+The fused path (k_fused, the c3 class: k <= 256, d <= 64) has two screens in
+the product library (km_set_screen): fp16x3 with the global bound and fp16x3
+with per-key bounds.  The diagnostic library (KM_LIB=diag) adds the fast
+screen (k_fused1: one fp16 MFMA per product against a balanced fp16 image,
+PAIRWISE bound; row as one fp16 part, or hi + lo), which lost end to end on
+every BASELINE shape and is not in the product build.  The choice is a cost
+choice, so each mode is forced here and held to the same bar as the automatic
+choice: labels equal to
 np.argmin(np.linalg.norm(C - x, axis=1)) (kmeans_spark.py:153-156) bit for
 bit, centroids and SSE at 1e-9 against the oracle (kmeans_spark.py:147-237).
 
@@ -21,9 +23,12 @@ import pytest
 
 from oracle import kmeans_oracle as orc
 
+from conftest import DIAG_LIB
+
 pytestmark = pytest.mark.gpu
 
-MODES = [0, 1, 2, 3]
+MODES = [0, 1, 2, 3] if DIAG_LIB else [0, 1]
+diag_only = pytest.mark.skipif(not DIAG_LIB, reason="fast screen: diagnostic library only (KM_LIB=diag)")
 
 
 def _km():
@@ -156,6 +161,7 @@ def test_duplicate_centroids_lowest_index(mode):
     assert not np.any(labels == 10) and not np.any(labels == 200)
 
 
+@diag_only
 def test_auto_policy_switches_to_fast_screen_and_stays_exact():
     # well separated blobs, one seed per blob: the fp16x3 batch queues almost
     # nothing, so the runtime moves the next batch to the fast screen (policy
@@ -191,6 +197,7 @@ def test_auto_policy_switches_to_fast_screen_and_stays_exact():
     np.testing.assert_array_equal(km.predict(X).to_numpy(), orc.assign(X, ref["centroids"])[0])
 
 
+@diag_only
 @pytest.mark.parametrize("mode", [2, 3])
 @pytest.mark.parametrize("n,d,k", [(20000, 32, 128), (9000, 48, 200)])
 def test_fast_modes_fall_back_outside_the_fast_shape(mode, n, d, k):
@@ -199,3 +206,14 @@ def test_fast_modes_fall_back_outside_the_fast_shape(mode, n, d, k):
     X = _blobs(n, d, k // 2, seed=d + k)
     C0 = X[np.random.default_rng(4).choice(n, k, replace=False)]
     _check(X, C0, mode)
+
+
+def test_product_library_rejects_fast_screens():
+    if DIAG_LIB:
+        pytest.skip("product library only")
+    from kmeans_amd import _lib
+    from kmeans_amd.engine import make_engine
+    from kmeans_amd.comm import Communicator
+    eng = make_engine(Communicator())
+    with pytest.raises(_lib.KmError, match="diagnostic build only"):
+        eng.set_screen(2)

@@ -296,10 +296,10 @@ def test_wide_rows_triple_ties_full_scan_vs_oracle(n, d, nb):
 
 @pytest.mark.parametrize("n,d,k,centers", [
     (20000, 16, 8, 8),          # c2 shape: small path, residuals fused in k_assign_small
-    (20000, 64, 256, 256),      # c3 shape: fused kernel, residuals in the k_sse pass
-    (12000, 32, 1024, 256),     # c4 shape: unfused MFMA path, k_stats + k_sse
+    (20000, 64, 256, 256),      # c3 shape: fused kernel, residuals in the same pass + resolvers
+    (12000, 32, 1024, 256),     # c4 shape: unfused MFMA path, residuals in k_stats
     (12000, 128, 4096, 512),    # c5 shape: label-sorted statistics, residuals fused in k_segsum
-    (5000, 64, 300, 60),        # unfused, LDS-range statistics + k_sse
+    (5000, 64, 300, 60),        # unfused, LDS-range statistics with residuals
 ])
 def test_tight_clusters_sse_vs_oracle(n, d, k, centers):
     # std 1e-3 in a +-1000 box: sum ||x||^2 is ~1e12 x the SSE.  The reference

@@ -43,10 +43,12 @@ def test_product_library_has_no_diagnostic_kernels():
     import subprocess
     from kmeans_amd import _lib
     syms = subprocess.run(["nm", "-C", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
-    fused = re.findall(r"k_fused<\d+, \d+, (?:true|false), (\d+), (?:true|false)>", syms)
+    fused = re.findall(r"k_fused<\d+, \d+, (?:true|false), (\d+), (?:true|false), (?:true|false)>", syms)
     mfma = re.findall(r"k_assign_mfma<\d+, \d+, (\d+), (?:true|false)>", syms)
     assert fused and mfma, "kernel symbols not found"
     assert set(fused) == {"0"} and set(mfma) == {"0"}, (set(fused), set(mfma))
+    # the fast-screen experiment (k_fused1, k_prep_bal) is diagnostic-only too
+    assert "k_fused1" not in syms and "k_prep_bal" not in syms
     assert "getenv" not in subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True,
                                           text=True, check=True).stdout
 
@@ -215,6 +217,52 @@ def test_driver_reproduces_reference_with_cpu_engine(golden, cpu_engine, name):
     np.testing.assert_allclose(km.sse_history, g["sse_history"], rtol=1e-9)
     assert_logs_match(out, g["stdout"])
     np.testing.assert_array_equal(labels, g["labels"])
+
+
+def test_failure_inside_a_batch_closes_it():
+    # an error between km_batch_begin and km_batch_end (here: the third
+    # assign of a batch) must still close the batch, or the device gate stays
+    # up and every later launch on the context is a silent no-op
+    ka = _ka()
+    import cpu_engine as ce
+
+    class Boom(RuntimeError):
+        pass
+
+    engines = []
+
+    class Flaky(ce.OracleEngine):
+        calls = 0
+
+        def assign_stats(self):
+            Flaky.calls += 1
+            if Flaky.calls == 3:
+                raise Boom("injected failure")
+            return super().assign_stats()
+
+        def batch_end(self, m):
+            self.closed = getattr(self, "closed", 0) + 1
+            return super().batch_end(m)
+
+    def factory(comm):
+        engines.append(Flaky(comm))
+        return engines[-1]
+
+    class K(ka.KMeans):
+        _engine_factory = staticmethod(factory)
+
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((400, 3))
+    km = K(k=3, max_iter=10, seed=1)
+    km.verbose = False
+    with pytest.raises(Boom):
+        km.fit(X)
+    eng = engines[-1]
+    assert eng.closed == 1 and not eng._batching
+    # the same model fits again afterwards (a new context, no open batch)
+    Flaky.calls = 10
+    km.fit(X)
+    assert km.centroids.shape == (3, 3) and np.all(np.isfinite(km.centroids))
 
 
 def test_predict_reuses_fit_rows_only_for_the_same_object(cpu_engine):
