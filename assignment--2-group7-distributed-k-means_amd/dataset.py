@@ -12,16 +12,20 @@ The reference receives a PySpark RDD of ``(d,)`` float arrays built by
   HBM (benchmarks; nothing on the host).
 
 ``place`` turns one into a ``Placement``: the global partition layout (needed
-by the takeSample policy) and this rank's contiguous block of partitions and
-rows.  With W ranks, rank r owns partitions ``[r*P//W, (r+1)*P//W)`` (a
-one-partition input is cut into W row blocks), so concatenating the ranks'
-predictions restores input order.
+by the takeSample policy) and this rank's contiguous block of rows.  With N
+rows over W ranks, rank r owns global rows ``[r*N//W, (r+1)*N//W)`` whatever
+the partition boundaries (the reference's own inputs have 1-4 partitions,
+kmeans_spark.py:418, 561-568, so whole partitions per rank would leave GPUs
+idle); a rank's block may start and end inside partitions.  The takeSample
+layout stays the dataset's own partitioning, so the sampled rows and the whole
+run are the same for any W; concatenating the ranks' predictions restores
+input order.
 
 Ingestion is sharded at the source: the layout comes from a count pass
 (for a PySpark RDD it runs on the executors: one ``(rows, width, dtype)``
 triple per partition reaches the rank), and each rank then materialises only
-its own partitions (``mapPartitionsWithIndex`` filtered to its block), so no
-rank holds another rank's rows.  Rows needed by index later (takeSample
+its own rows (``mapPartitionsWithIndex`` slicing each overlapping partition to
+the rank's row range), so no rank holds another rank's rows.  Rows needed by index later (takeSample
 picks, kmeans_spark.py:72, 196) are gathered from the ranks' HBM
 (``LloydRunner.rows``).
 
@@ -204,58 +208,62 @@ def _layout(rdd) -> Tuple[List[int], Optional[int], Any]:
                     f"ndarray or DeviceBlobs")
 
 
-def _own_rows(rdd, lo: int, hi: int, d: int, row_range: Optional[Tuple[int, int]] = None) -> np.ndarray:
-    """This rank's rows: partitions [lo, hi), or rows [a, b) of the single
-    partition 0 (row_range).  Only they are materialised / transferred."""
+def _segments(sizes: Sequence[int], a: int, b: int) -> List[Tuple[int, int, int]]:
+    """Global rows [a, b) as (partition, first, stop) pieces, in row order."""
+    out, start = [], 0
+    for i, n in enumerate(sizes):
+        lo, hi = max(a, start), min(b, start + n)
+        if lo < hi:
+            out.append((i, lo - start, hi - start))
+        start += n
+    return out
+
+
+def _own_rows(rdd, segs: List[Tuple[int, int, int]], d: int) -> np.ndarray:
+    """This rank's rows: the given partition pieces.  Only they are
+    materialised / transferred."""
     if isinstance(rdd, np.ndarray):
-        a, b = row_range if row_range else (0, rdd.shape[0])
-        return rdd[a:b]
+        return np.concatenate([rdd[lo:hi] for _, lo, hi in segs]) if segs else np.zeros((0, d))
     if isinstance(rdd, LocalRDD):
-        if row_range:
-            p = rdd.partition_array(0)
-            return p[row_range[0]:row_range[1]] if p is not None else np.zeros((0, d))
-        mine = [rdd.partition_array(i) for i in range(lo, hi)]
-        mine = [m.reshape(len(m), d) for m in mine if m is not None]
+        mine = []
+        for i, lo, hi in segs:
+            p = rdd.partition_array(i)
+            if p is not None:
+                mine.append(p[lo:hi].reshape(hi - lo, d))
         return np.concatenate(mine) if mine else np.zeros((0, d))
+    want = {i: (lo, hi) for i, lo, hi in segs}
 
-    if row_range:
-        a, b = row_range
-
-        def keep(i, it):
-            return itertools.islice(it, a, b) if i == 0 else iter(())
-    else:
-        def keep(i, it):
-            return it if lo <= i < hi else iter(())
-    rows = rdd.mapPartitionsWithIndex(keep).collect()
+    def keep(i, it):
+        if i not in want:
+            return iter(())
+        lo, hi = want[i]
+        return itertools.islice(it, lo, hi)
+    rows = rdd.mapPartitionsWithIndex(keep).collect()  # partitions come back in index order
     return np.asarray(rows).reshape(len(rows), d) if rows else np.zeros((0, d))
+
+
+def rank_rows(n: int, world: int, rank: int) -> Tuple[int, int]:
+    """Global row range [a, b) of a rank: balanced to one row."""
+    return (rank * n) // world, ((rank + 1) * n) // world
 
 
 def place(rdd, comm) -> Placement:
     if isinstance(rdd, DeviceBlobs):
-        W, r = comm.world, comm.rank
-        sizes = [((i + 1) * rdd.n) // W - (i * rdd.n) // W for i in range(W)]
-        row0 = (r * rdd.n) // W
+        a, b = rank_rows(rdd.n, comm.world, comm.rank)
         P = max(1, int(rdd.partitions))
         layout = [((i + 1) * rdd.n) // P - (i * rdd.n) // P for i in range(P)]
-        return Placement(global_sizes=layout, local_rows=None, row0=row0, n_local=sizes[r], n_global=rdd.n,
+        return Placement(global_sizes=layout, local_rows=None, row0=a, n_local=b - a, n_global=rdd.n,
                          d=rdd.d, dtype=np.float64, blobs=rdd)
     sizes, d, dtype = _layout(rdd)
     if d is None:
         raise ValueError("Not enough data points (0) to initialize clusters")
     if not np.issubdtype(np.dtype(dtype), np.floating):
         dtype = np.float64
-    W, r = comm.world, comm.rank
-    if len(sizes) == 1 and W > 1:
-        # one partition: cut into W row blocks (the takeSample layout is still ONE partition)
-        n = sizes[0]
-        a, b = (r * n) // W, ((r + 1) * n) // W
-        local = _own_rows(rdd, 0, 1, d, row_range=(a, b))
-        row0 = a
-    else:
-        P = len(sizes)
-        lo, hi = (r * P) // W, ((r + 1) * P) // W
-        local = _own_rows(rdd, lo, hi, d)
-        row0 = int(sum(sizes[:lo]))
+    # balanced row blocks across partition boundaries (the takeSample layout
+    # stays the dataset's partitions)
+    a, b = rank_rows(int(sum(sizes)), comm.world, comm.rank)
+    local = _own_rows(rdd, _segments(sizes, a, b), d)
+    row0 = a
     if local.ndim != 2:
         local = local.reshape(len(local), d)
     return Placement(global_sizes=sizes, local_rows=local, row0=row0, n_local=len(local),

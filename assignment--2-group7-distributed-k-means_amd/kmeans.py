@@ -194,7 +194,13 @@ class LloydRunner:
 
 
 class LabelsRDD(LocalRDD):
-    """``predict``'s result: an RDD-like of Python ints in input order."""
+    """``predict``'s result: an RDD-like of Python ints in input order.
+
+    The labels stay sharded (each rank holds its own rows' labels, its row
+    block of the input) until an action needs them all: ``collect()`` /
+    ``to_numpy()`` gather them (every rank runs the driver program, so every
+    rank gets the whole list, as Spark's driver does), ``count()`` sums the
+    shard lengths, ``local()`` is this rank's shard with no communication."""
 
     def __init__(self, local_labels: np.ndarray, comm: Communicator):
         self._local = local_labels
@@ -213,10 +219,16 @@ class LabelsRDD(LocalRDD):
         return self._gather().tolist()
 
     def count(self) -> int:
-        return int(len(self._gather()))
+        if self._comm.world > 1:
+            return int(self._comm.allreduce_np(np.array([float(len(self._local))]))[0])
+        return int(len(self._local))
 
     def getNumPartitions(self) -> int:
-        return 1
+        return self._comm.world
+
+    def local(self) -> np.ndarray:
+        """This rank's labels (rows [row0, row0 + n_local) of the input)."""
+        return self._local
 
     def to_numpy(self) -> np.ndarray:
         return self._gather()

@@ -14,7 +14,7 @@ import re
 import numpy as np
 import pytest
 
-from conftest import GOLDEN_CASES
+from conftest import F32_CASES, GOLDEN_CASES, check_float32_run
 from oracle import kmeans_oracle as orc
 
 pytestmark = pytest.mark.gpu
@@ -29,7 +29,7 @@ def _km():
     return kmeans_amd
 
 
-def _fit_product(g, inject=True, slices=None):
+def _fit_product(g, inject=True, slices=None, dtype=None):
     ka = _km()
     init = g["init"]
 
@@ -43,7 +43,7 @@ def _fit_product(g, inject=True, slices=None):
             return int(g["time_seed"])
 
     sc = ka.LocalContext()
-    rdd = sc.parallelize(g["X"], slices or int(g["slices"]))
+    rdd = sc.parallelize(g["X"] if dtype is None else g["X"].astype(dtype), slices or int(g["slices"]))
     km = Pinned(k=int(g["k"]), max_iter=int(g["max_iter"]), tolerance=float(g["tol"]), seed=int(g["seed"]),
                 compute_sse=bool(g["sse"]))
     buf = io.StringIO()
@@ -68,6 +68,20 @@ def assert_logs_match(ours, ref):
         assert _NUM.sub("#", x) == _NUM.sub("#", y), (x, y)
         for u, v in zip(_NUM.findall(x), _NUM.findall(y)):
             assert abs(float(u) - float(v)) <= 2 * 10 ** -len(v.split(".")[1]) + 1e-9 * abs(float(v)), (x, y)
+
+
+@pytest.mark.parametrize("name", F32_CASES)
+def test_float32_rows_meet_the_bars_against_the_reference_float32_run(golden, name):
+    # the reference on float32 rows computes in float32; the product in
+    # float64 on the same rows (centroids returned as float32)
+    g = golden(name)
+    km, out, labels = _fit_product(g, dtype=np.float32)
+    check_float32_run(g, km.centroids, km.sse_history, labels, out)
+    # and the product's own contract: the float64 run on those rows
+    ref = orc.lloyd_fit(g["X"], int(g["k"]), int(g["max_iter"]), float(g["tol"]), int(g["seed"]), True,
+                        int(g["slices"]), init_centroids=g["init"], empty_seed=lambda: int(g["time_seed"]))
+    np.testing.assert_allclose(km.centroids, ref["centroids"].astype(np.float32), rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)
 
 
 @pytest.mark.parametrize("name", GOLDEN_CASES)

@@ -142,9 +142,22 @@ def test_placement_partitions_and_order():
     rdd = ka.LocalContext().parallelize(X, 5)
     pls = [place(rdd, FakeComm(r, 2)) for r in range(2)]
     assert pls[0].global_sizes == [200] * 5
-    assert [p.n_local for p in pls] == [400, 600]
+    # balanced to one row across partition boundaries (rank 1 starts inside
+    # partition 2); the takeSample layout stays the 5 partitions
+    assert [p.n_local for p in pls] == [500, 500]
     np.testing.assert_array_equal(np.concatenate([p.local_rows for p in pls]), X)
-    assert pls[1].row0 == 400
+    assert pls[1].row0 == 500 and pls[1].global_sizes == [200] * 5
+    # the reference's own inputs have 1-4 partitions (kmeans_spark.py:418,
+    # 561-568): 8 ranks over a 4-partition RDD leave no rank idle
+    r4 = ka.LocalContext().parallelize(X, 4)
+    p8 = [place(r4, FakeComm(r, 8)) for r in range(8)]
+    assert [p.n_local for p in p8] == [125] * 8
+    np.testing.assert_array_equal(np.concatenate([p.local_rows for p in p8]), X)
+    # uneven partitions (one empty) and more ranks than rows in a partition
+    r5 = ka.LocalRDD([X[:7], X[7:7], X[7:300], X[300:]])
+    p3 = [place(r5, FakeComm(r, 3)) for r in range(3)]
+    assert [p.n_local for p in p3] == [333, 333, 334]
+    np.testing.assert_array_equal(np.concatenate([p.local_rows for p in p3]), X)
     # a bare array is one takeSample partition, cut into row blocks per rank
     pa = [place(X, FakeComm(r, 3)) for r in range(3)]
     assert pa[0].global_sizes == [1000]
@@ -217,6 +230,33 @@ def test_driver_reproduces_reference_with_cpu_engine(golden, cpu_engine, name):
     np.testing.assert_allclose(km.sse_history, g["sse_history"], rtol=1e-9)
     assert_logs_match(out, g["stdout"])
     np.testing.assert_array_equal(labels, g["labels"])
+
+
+@pytest.mark.parametrize("name", ["f32_test_a", "f32_c1", "f32_c3_small", "f32_empty"])
+def test_float32_rows_cpu_engine_vs_reference_float32(golden, cpu_engine, name):
+    # host logic with a float32 RDD (centroid dtype, logs, SSE history)
+    # through the CPU engine, against the reference's float32 run
+    from conftest import check_float32_run
+    ka = _ka()
+    g = golden(name)
+    init = g["init"]
+
+    class Pinned(ka.KMeans):
+        def _initialize_centroids(self, run):
+            return init.copy()
+
+        def _empty_seed(self):
+            return int(g["time_seed"])
+
+    sc = ka.LocalContext()
+    rdd = sc.parallelize(g["X"].astype(np.float32), int(g["slices"]))
+    km = Pinned(k=int(g["k"]), max_iter=int(g["max_iter"]), tolerance=float(g["tol"]), seed=int(g["seed"]),
+                compute_sse=bool(g["sse"]))
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        km.fit(rdd, sc)
+    labels = np.array(km.predict(rdd, sc).collect())
+    check_float32_run(g, km.centroids, km.sse_history, labels, buf.getvalue())
 
 
 def test_failure_inside_a_batch_closes_it():
@@ -429,7 +469,7 @@ def _shard_rank_main(rank, world, port, q):
                        compute_sse=bool(g["sse"]))
         km.verbose = False
         km.fit(rdd)
-        res["spark"] = (km.centroids, km.sse_history, sorted(set(rdd.log)))
+        res["spark"] = (km.centroids, km.sse_history, sorted(set(e for e in rdd.log if e[1])))
 
         # the package's LocalRDD: only this rank's partitions are materialised
         touched = []
@@ -452,7 +492,7 @@ def _shard_rank_main(rank, world, port, q):
 
 def test_two_ranks_ingest_only_their_own_partitions(golden):
     # sharded ingestion (kmeans_spark.py:256 rdd.cache() -> HBM): rank r
-    # materialises only partitions [r P/W, (r+1) P/W); the fit is unchanged
+    # materialises only global rows [r N/W, (r+1) N/W); the fit is unchanged
     import torch.multiprocessing as mp
     g = golden("test_d")
     ctx = mp.get_context("spawn")
@@ -465,11 +505,14 @@ def test_two_ranks_ingest_only_their_own_partitions(golden):
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
+    from kmeans_amd.dataset import _segments, rank_rows
     for rank, P, sizes, r in res:
-        own = list(range((rank * P) // 2, ((rank + 1) * P) // 2))
+        segs = _segments(sizes, *rank_rows(sum(sizes), 2, rank))
+        own = [i for i, _, _ in segs]
         C, sse, log = r["spark"]
-        assert [i for i, _ in log] == [i for i in own if sizes[i]], (rank, log)
-        assert all(cnt == sizes[i] for i, cnt in log)
+        # exactly this rank's rows came back: its row block, cut at the
+        # partition boundaries it spans
+        assert log == [(i, hi - lo) for i, lo, hi in segs], (rank, log)
         np.testing.assert_allclose(C, g["centroids"], rtol=1e-9, atol=1e-9)
         np.testing.assert_allclose(sse, g["sse_history"], rtol=1e-9)
         C2, sse2, touched = r["local"]
