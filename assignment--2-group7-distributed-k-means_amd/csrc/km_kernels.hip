@@ -1716,6 +1716,488 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Software-pipelined fused kernel (the c3 class with statistics, no SSE): the
+// same screen, bound, labels, queue and float64 sums as k_fused, arranged so
+// that one wave per SIMD keeps the matrix pipe busy.  In k_fused a tile's
+// split, merge and 33 LDS atomics run between MFMA blocks, serialised with
+// them (MFMA busy 49%, VALU 44%).  Here, while the MFMAs
+// of tile t run:
+//   * the sums of tile t-1 fill the gaps of the first half of the blocks: the
+//     rows of tile t-1 are re-read (L2-resident: loaded one tile earlier)
+//     instead of being held in 32 VGPRs, their loads issued before the next
+//     tile's HBM loads so the in-order vmcnt lets those stay in flight;
+//     rows that are not summed here (queued for the resolvers, or past the
+//     end) add into a discard column KP of the table, so the region has no
+//     branch (a branch would end the scheduling region);
+//   * the split of tile t+1 fills the gaps of the second half, into the
+//     other of two ping-pong B-operand sets.
+// What stays between blocks is the last block's keys and the merge / bound /
+// label / queue of tile t.
+// ---------------------------------------------------------------------------
+// STAMP (diagnostic build, KM_ABLATE=9): s_memtime phase stamps per tile
+// (head = loads + block 0, region = blocks 1 .. NB-1, tail = last keys +
+// merge + queue), the wave's whole-kernel cycles and s_memrealtime ticks
+template <int NS, int NB, bool REF, bool STAMP = false>
+__global__ __launch_bounds__(256, 1) void k_fusedp(FusedArgs A) {
+  if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
+  constexpr int DP = 16 * NS;
+  constexpr int KP = 32 * NB;
+  constexpr int WAVES = 4;
+  constexpr int B = ceil_log2_c(KP);
+  static_assert(B >= 3 && B - 2 <= 12, "index bits");
+  static_assert(NB >= 2, "pipelined blocks");
+  constexpr uint32_t maskq = (1u << (B - 2)) - 1u;
+  constexpr int TS = KP + 1;  // sum table row stride: column KP discards
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* sCn = reinterpret_cast<float*>(smem);              // ||c||^2 s^2 [KP]
+  double* tab = reinterpret_cast<double*>(smem + KP * 4);   // [DP + 1][TS]
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  for (int i = threadIdx.x; i < KP; i += WAVES * 64) sCn[i] = A.cn2s[i];
+  for (int i = threadIdx.x; i < (DP + 1) * TS; i += WAVES * 64) tab[i] = 0.0;
+  f16x8 Ahi[NB][NS], Alo[NB][NS];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      Ahi[b][t] = __builtin_bit_cast(f16x8, A.ChiF[(b * NS + t) * 64 + lane]);
+      Alo[b][t] = __builtin_bit_cast(f16x8, A.CloF[(b * NS + t) * 64 + lane]);
+    }
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int t = 0; t < NS; ++t) asm volatile("" : "+a"(Ahi[b][t]), "+a"(Alo[b][t]));
+  __syncthreads();
+
+  const float s = mfma_scale(*A.xabs, *A.cabs);
+  const float alpha = A.bnd[0], beta = A.bnd[1];
+  const float rho = __builtin_ldexpf(1.0f, B - 2 - 23) * 1.01f;
+  const int64_t n = A.n;
+  const int64_t ntiles = (n + 31) / 32;
+  const uint32_t gw = blockIdx.x * WAVES + wave;
+  QEntry* wq = A.queue + (size_t)gw * A.seg;
+  uint32_t qn = 0, qf = 0;
+  const int64_t tstride = (int64_t)gridDim.x * WAVES;
+  const float4* cnl = reinterpret_cast<const float4*>(sCn + 4 * h);
+
+  // rows of a tile (clamped to row n - 1 past the end: every path has the
+  // same loads in flight)
+  auto load_rows = [&](int64_t tile, float4 (&xq)[NS][2]) {
+    const int64_t row = tile * 32 + r;
+    const int64_t rr = row < n ? row : (n - 1);
+    const float* xr = A.X + rr * DP + 8 * h;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      xq[t][0] = *reinterpret_cast<const float4*>(xr + 16 * t);
+      xq[t][1] = *reinterpret_cast<const float4*>(xr + 16 * t + 4);
+    }
+  };
+  auto load_xn = [&](int64_t tile) {
+    const int64_t row = tile * 32 + r;
+    return A.xnorm[row < n ? row : (n - 1)];
+  };
+  // B operand chunk t: lane (r, h) holds features [16t + 8h, +8) of point r,
+  // xs = hi + lo (fp16, RN), one v_fma_mix per element for lo (as k_fused)
+  auto split_chunk = [&](const float4 (&xq)[NS][2], int t, f16x8& bh, f16x8& bl) {
+    // opaque copies: otherwise the vectoriser hoists the x * s products next
+    // to the loads, which then wait for HBM at the top of the tile
+    float xv[8] = {xq[t][0].x, xq[t][0].y, xq[t][0].z, xq[t][0].w,
+                   xq[t][1].x, xq[t][1].y, xq[t][1].z, xq[t][1].w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) asm("" : "+v"(xv[e]));
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      const float xs0 = xv[e] * s, xs1 = xv[e + 1] * s;
+      const f16x2 hp = {(_Float16)xs0, (_Float16)xs1};
+      uint32_t lp;
+      asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
+          "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+          : "=&v"(lp)
+          : "v"(__builtin_bit_cast(uint32_t, hp)), "v"(xs0), "v"(xs1));
+      const f16x2 lo = __builtin_bit_cast(f16x2, lp);
+      bh[e] = hp[0];
+      bh[e + 1] = hp[1];
+      bl[e] = lo[0];
+      bl[e + 1] = lo[1];
+    }
+  };
+  // sums of chunk t of the previous tile: 8 features of its row into the
+  // table column plab (KP: discard)
+  auto sum_chunk = [&](const float4 (&xq)[NS][2], int t, int plab) {
+    double* tp = tab + (size_t)(16 * t + 8 * h) * TS + plab;
+    const float xe[8] = {xq[t][0].x, xq[t][0].y, xq[t][0].z, xq[t][0].w,
+                         xq[t][1].x, xq[t][1].y, xq[t][1].z, xq[t][1].w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      // the conversion through inline asm: as plain (double) the vectoriser
+      // hoists all 32 conversions next to the loads (64 more live VGPRs and
+      // a vmcnt(0) in front of the next tile's HBM loads)
+      double v;
+      asm("v_cvt_f64_f32 %0, %1" : "=v"(v) : "v"(xe[e]));
+      atomicAdd(tp + (size_t)e * TS, v);
+    }
+  };
+
+  // the tile's B operands (ping-pong), the next tile's rows, previous tile
+  f16x8 bA[NS], lA[NS], bB[NS], lB[NS];
+  float4 xnext[NS][2];
+  float xnA = 0.0f, xnB = 0.0f;
+  int64_t prow = (int64_t)gw * 32 + r;  // re-read address of the previous tile's row (clamped)
+  int plab = KP;                        // previous tile: column summed into (KP: discard)
+  int pcnt = KP;                        // count column (h == 0 lanes only), KP: discard
+  unsigned long long st_acc[3] = {0, 0, 0}, st_t = 0;
+  const unsigned long long st_k0 = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+  const unsigned long long st_r0 = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
+  auto stamp = [&](int slot) {
+    if constexpr (STAMP) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long tn = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      if (slot >= 0) st_acc[slot] += tn - st_t;
+      st_t = tn;
+    }
+  };
+
+  auto tile_step = [&](int64_t tile, f16x8 (&bh)[NS], f16x8 (&bl)[NS], f16x8 (&bhn)[NS], f16x8 (&bln)[NS],
+                       float xn, float& xn_next) {
+    stamp(-1);
+    const int64_t row = tile * 32 + r;
+    const bool valid = row < n;
+    // previous tile's rows (L2), then the next tile's (HBM): the in-order
+    // vmcnt waits for the re-read alone
+    float4 xprev[NS][2];
+    {
+      const float* xr = A.X + (prow < n ? prow : (n - 1)) * DP + 8 * h;
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+        xprev[t][0] = *reinterpret_cast<const float4*>(xr + 16 * t);
+        xprev[t][1] = *reinterpret_cast<const float4*>(xr + 16 * t + 4);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the re-read older than the HBM loads
+    load_rows(tile + tstride, xnext);
+    xn_next = load_xn(tile + tstride);
+    __builtin_amdgcn_sched_barrier(0);
+
+    float a1[4], a2[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a1[c] = a2[c] = FLT_MAX;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int t = 0; t < NS; ++t) asm volatile("" : "+a"(Ahi[b][t]), "+a"(Alo[b][t]));
+    auto cn_init = [&](int blk) {
+      f32x16 acc;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 cv = cnl[8 * blk + 2 * g4];
+        acc[4 * g4 + 0] = cv.x;
+        acc[4 * g4 + 1] = cv.y;
+        acc[4 * g4 + 2] = cv.z;
+        acc[4 * g4 + 3] = cv.w;
+      }
+      return acc;
+    };
+    auto mfma_block = [&](f32x16 acc, int blk) {
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bl[t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Alo[blk][t], bh[t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bh[t], acc, 0, 0, 0);
+      }
+      return acc;
+    };
+    // one MFMA of block blk: step i = 3 t + (0: hi x lo, 1: lo x hi, 2: hi x hi)
+    auto mfma_step = [&](f32x16& acc, int blk, int i) {
+      const int t = i / 3, w = i % 3;
+      if (w == 0) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bl[t], acc, 0, 0, 0);
+      if (w == 1) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Alo[blk][t], bh[t], acc, 0, 0, 0);
+      if (w == 2) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bh[t], acc, 0, 0, 0);
+    };
+    // keys of one chain pair p of block blk (registers ra, ra + 4 of chain
+    // c): new best = min3(best, ka, kb), new second = min(second, med3(...));
+    // keys carry (j >> 2) without the lane-half bit h: 8 blk + 2 (reg >> 2),
+    // an inline constant for KP <= 256 (no index registers); h is put back
+    // in pidx.  Keys of the two halves can then tie exactly only between
+    // different centroids of equal truncated score, which leaves no
+    // certificate (k2 - k1 = 0): such a row is queued, its label and sums
+    // come from the resolvers, and every decision that sums a row here
+    // (kind 0) depends on the key values alone, identical in both halves
+    auto key_pair = [&](const f32x16& acc, int blk, int pp) {
+      const int c = pp & 3, ra = 8 * (pp >> 2) + c, rb = ra + 4;
+      const float ka = __uint_as_float((__float_as_uint(acc[ra]) & ~maskq) | (uint32_t)(8 * blk + 2 * (ra >> 2)));
+      const float kb = __uint_as_float((__float_as_uint(acc[rb]) & ~maskq) | (uint32_t)(8 * blk + 2 * (rb >> 2)));
+      const float tm = __builtin_amdgcn_fmed3f(a1[c], ka, kb);
+      a1[c] = __builtin_fminf(__builtin_fminf(a1[c], ka), kb);
+      a2[c] = __builtin_fminf(a2[c], tm);
+    };
+    auto cn_part = [&](f32x16& acc, int blk, int g4) {
+      const float4 cv = cnl[8 * blk + 2 * g4];
+      acc[4 * g4 + 0] = cv.x;
+      acc[4 * g4 + 1] = cv.y;
+      acc[4 * g4 + 2] = cv.z;
+      acc[4 * g4 + 3] = cv.w;
+    };
+    // One element pair (e, e+1) of chunk t: sums of the previous tile (two
+    // features into the table) or the split of the next tile
+    auto sum_pair = [&](int t, int e) {
+      double* tp = tab + (size_t)(16 * t + 8 * h + e) * TS + plab;
+      const float x0 = (e & 4) ? ((e & 2) ? xprev[t][1].z : xprev[t][1].x) : ((e & 2) ? xprev[t][0].z : xprev[t][0].x);
+      const float x1 = (e & 4) ? ((e & 2) ? xprev[t][1].w : xprev[t][1].y) : ((e & 2) ? xprev[t][0].w : xprev[t][0].y);
+      double v0, v1;
+      // the conversions through inline asm: as plain (double) the vectoriser
+      // hoists all 32 next to the loads (64 more live VGPRs, and a vmcnt(0)
+      // in front of the next tile's HBM loads)
+      asm("v_cvt_f64_f32 %0, %1" : "=v"(v0) : "v"(x0));
+      asm("v_cvt_f64_f32 %0, %1" : "=v"(v1) : "v"(x1));
+      atomicAdd(tp, v0);
+      atomicAdd(tp + TS, v1);
+    };
+    auto split_pair = [&](int t, int e) {
+      float x0 = (e & 4) ? ((e & 2) ? xnext[t][1].z : xnext[t][1].x) : ((e & 2) ? xnext[t][0].z : xnext[t][0].x);
+      float x1 = (e & 4) ? ((e & 2) ? xnext[t][1].w : xnext[t][1].y) : ((e & 2) ? xnext[t][0].w : xnext[t][0].y);
+      // opaque: otherwise the products are hoisted next to the HBM loads
+      asm("" : "+v"(x0));
+      asm("" : "+v"(x1));
+      const float xs0 = x0 * s, xs1 = x1 * s;
+      const f16x2 hp = {(_Float16)xs0, (_Float16)xs1};
+      uint32_t lp;
+      asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
+          "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+          : "=&v"(lp)
+          : "v"(__builtin_bit_cast(uint32_t, hp)), "v"(xs0), "v"(xs1));
+      const f16x2 lo = __builtin_bit_cast(f16x2, lp);
+      bhn[t][e] = hp[0];
+      bhn[t][e + 1] = hp[1];
+      bln[t][e] = lo[0];
+      bln[t][e + 1] = lo[1];
+    };
+
+    // Explicit schedule of one block (M = 3 NS MFMAs, each followed by its
+    // filler work and a sched_barrier, so the issue order is the program
+    // order): key pair p of the previous block at step 2 + p (M - 4) / 8
+    // (the first two steps cover the previous block's MFMA latency); the
+    // next block's accumulator init, registers 4 g4 .. 4 g4 + 3, right after
+    // the last key pair that reads them; fillers at the other steps.  The
+    // tile's fillers -- NS sum chunks of the previous tile, then NS split
+    // chunks of the next -- are spread over blocks 2 .. NB-1 (sums first: the
+    // re-read needs an L2 round trip, the split waits for HBM).
+    constexpr int M = 3 * NS;
+    constexpr int F0 = NB >= 4 ? 2 : 1;  // first block with fillers
+    auto key_step = [&](int pp) { return 2 + (pp * (M - 4 > 0 ? M - 4 : 1)) / 8; };
+    f32x16 accs[2];
+    auto run_block = [&](int blk) {
+      f32x16& acc = accs[blk & 1];
+      f32x16& prev = accs[(blk - 1) & 1];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        mfma_step(acc, blk, i);
+#pragma unroll
+        for (int pp = 0; pp < 8; ++pp)
+          if (key_step(pp) == i || (pp == 7 && i == M - 1 && key_step(7) >= M)) key_pair(prev, blk - 1, pp);
+        if (blk + 1 < NB) {
+          if (i == key_step(3) || (i == M - 1 && key_step(3) >= M)) {
+            cn_part(prev, blk + 1, 0);
+            cn_part(prev, blk + 1, 1);
+          }
+          if (i == key_step(7) || (i == M - 1 && key_step(7) >= M)) {
+            cn_part(prev, blk + 1, 2);
+            cn_part(prev, blk + 1, 3);
+          }
+        }
+        // filler slots: the steps without a key pair; chunk u of the tile's
+        // 2 NS filler chunks (4 element pairs each) belongs to block
+        // F0 + u (NB - F0) / (2 NS)
+        bool keyed = false;
+#pragma unroll
+        for (int pp = 0; pp < 8; ++pp) keyed |= key_step(pp) == i;
+        if (!keyed || M <= 6) {
+          int slot = 0, nslots = 0;
+#pragma unroll
+          for (int q = 0; q < M; ++q) {
+            bool kq = false;
+#pragma unroll
+            for (int pp = 0; pp < 8; ++pp) kq |= key_step(pp) == q;
+            if (!kq || M <= 6) {
+              if (q < i) ++slot;
+              ++nslots;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 2 * NS; ++u) {
+            if (F0 + (u * (NB - F0)) / (2 * NS) != blk) continue;
+            // this block's chunks, in order; element pairs spread over its slots
+            int first = 0, nch = 0;
+#pragma unroll
+            for (int v = 0; v < 2 * NS; ++v)
+              if (F0 + (v * (NB - F0)) / (2 * NS) == blk) {
+                if (v < u) ++first;
+                ++nch;
+              }
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+              const int item = (first * 4 + e / 2);
+              if ((item * nslots) / (nch * 4) != slot) continue;
+              if (u < NS) {
+                sum_pair(u, e);
+                if (u == 0 && e == 0) atomicAdd(tab + (size_t)DP * TS + pcnt, 1.0);  // count row (h = 1: discard)
+              } else {
+                split_pair(u - NS, e);
+              }
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    accs[0] = cn_init(0);
+    accs[1] = cn_init(1);
+    accs[0] = mfma_block(accs[0], 0);
+    __builtin_amdgcn_sched_barrier(0);
+    stamp(0);
+#pragma unroll
+    for (int blk = 1; blk < NB; ++blk) run_block(blk);
+    stamp(1);
+#pragma unroll
+    for (int pp = 0; pp < 8; ++pp) key_pair(accs[(NB - 1) & 1], NB - 1, pp);
+
+    // merge, bound, label, queue (as k_fused)
+    auto pidx = [&](float key, int c) { return ((__float_as_uint(key) & maskq) << 2) | (uint32_t)(4 * h + c); };
+    float k1 = a1[0], k2 = a2[0], k3 = a2[0];
+    uint32_t p1 = pidx(a1[0], 0), p2 = pidx(a2[0], 0);
+    {
+      float m1 = a1[2], m2 = a2[2], m3 = a2[2];
+      uint32_t q1 = pidx(a1[2], 2), q2 = pidx(a2[2], 2);
+      merge3(k1, k2, k3, p1, p2, a1[1], a2[1], a2[1], pidx(a1[1], 1), pidx(a2[1], 1));
+      merge3(m1, m2, m3, q1, q2, a1[3], a2[3], a2[3], pidx(a1[3], 3), pidx(a2[3], 3));
+      merge3(k1, k2, k3, p1, p2, m1, m2, m3, q1, q2);
+    }
+    {
+      uint32_t K1, Q1, K2, Q2, K3, Q3, P1, R1, P2, R2;
+      perm_halves(__float_as_uint(k1), K1, Q1);
+      perm_halves(__float_as_uint(k2), K2, Q2);
+      perm_halves(__float_as_uint(k3), K3, Q3);
+      perm_halves(p1, P1, R1);
+      perm_halves(p2, P2, R2);
+      k1 = __uint_as_float(K1);
+      k2 = __uint_as_float(K2);
+      k3 = __uint_as_float(K3);
+      p1 = P1;
+      p2 = P2;
+      merge3(k1, k2, k3, p1, p2, __uint_as_float(Q1), __uint_as_float(Q2), __uint_as_float(Q3), R1, R2);
+    }
+    const bool same_chain = ((p1 ^ p2) & 7u) == 0u;
+    const float B0 = fmaf(alpha, xn, beta);
+    const float thr2 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k2));
+    const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k3));
+    uint32_t kind = 0;
+    if (!(k2 - k1 > thr2)) kind = (same_chain || !(k3 - k1 > thr3)) ? 2u : 1u;
+    float u1 = 0.0f;
+    KeyBounds kb;
+    const bool refine = REF && __ballot(kind != 0u) != 0ull;
+    if (refine) {
+      kb = key_bounds(xn * s, *A.xabs * s, DP, rho);
+      if (kind != 0u) {
+        u1 = kb.upper(k1);
+        if (u1 < kb.lower(k2))
+          kind = 0u;
+        else if (kind == 2u && !same_chain && kb.lower(k3) > u1)
+          kind = 1u;
+      }
+    }
+    if (__ballot(kind == 2u && same_chain) != 0ull) {
+      const uint32_t cs = p1 & 7u;
+      float o = FLT_MAX;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t v0, v1;
+        perm_halves(__float_as_uint(a1[c]), v0, v1);
+        if ((uint32_t)c != cs) o = kmin(o, __uint_as_float(v0));
+        if ((uint32_t)(4 + c) != cs) o = kmin(o, __uint_as_float(v1));
+      }
+      const float thr3x = 2.0f * B0 + rho * (fabsf(k1) + fabsf(o));
+      if (kind == 2u && same_chain && (o - k1 > thr3x || (REF && kb.lower(o) > u1))) kind = 3u;
+    }
+    const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
+    if (h == 0 && valid) A.labels[row] = lab;
+    const bool enq = (h == 0) && valid && (kind != 0);
+    const uint64_t m = __ballot(enq);
+    if (m) {
+      const uint64_t m1 = __ballot(enq && kind == 1);
+      const uint64_t m2 = m & ~m1;
+      const uint64_t below = (1ull << lane) - 1ull;
+      if (enq) {
+        QEntry q;
+        q.row = (uint32_t)row;
+        q.i1 = p1;
+        q.i2 = p2;
+        q.kind = kind;
+        const uint32_t pos = (kind == 1) ? qn + (uint32_t)__popcll(m1 & below)
+                                         : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
+        wq[pos] = q;
+      }
+      qn += (uint32_t)__popcll(m1);
+      qf += (uint32_t)__popcll(m2);
+    }
+    // this tile is summed during the next one's MFMAs (or by the epilogue)
+    prow = row;
+    plab = (valid && kind == 0u) ? lab : KP;
+    pcnt = (valid && kind == 0u && h == 0) ? lab : KP;
+    stamp(2);
+  };
+
+  // prologue: the first tile's rows and split (not overlapped)
+  const int64_t t0 = gw;
+  if (t0 < ntiles) {
+    load_rows(t0, xnext);
+    xnA = load_xn(t0);
+#pragma unroll
+    for (int t = 0; t < NS; ++t) split_chunk(xnext, t, bA[t], lA[t]);
+  }
+  for (int64_t tile = t0; tile < ntiles; tile += 2 * tstride) {
+    tile_step(tile, bA, lA, bB, lB, xnA, xnB);
+    if (tile + tstride >= ntiles) break;
+    tile_step(tile + tstride, bB, lB, bA, lA, xnB, xnA);
+  }
+  // epilogue: the last tile's sums
+  if (t0 < ntiles) {
+    float4 xl[NS][2];
+    const float* xr = A.X + (prow < n ? prow : (n - 1)) * DP + 8 * h;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      xl[t][0] = *reinterpret_cast<const float4*>(xr + 16 * t);
+      xl[t][1] = *reinterpret_cast<const float4*>(xr + 16 * t + 4);
+    }
+#pragma unroll
+    for (int t = 0; t < NS; ++t) sum_chunk(xl, t, plab);
+    atomicAdd(tab + (size_t)DP * TS + pcnt, 1.0);
+  }
+  if (lane == 0) {
+    A.qcount[2 * gw] = qn;
+    A.qcount[2 * gw + 1] = qf;
+  }
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      for (int i = 0; i < 3; ++i) atomicAdd(&g_stamp[i], st_acc[i]);
+      atomicAdd(&g_stamp[3], __builtin_amdgcn_s_memtime() - st_k0);
+      atomicAdd(&g_stamp[4], __builtin_amdgcn_s_memrealtime() - st_r0);
+      atomicAdd(&g_stamp[5], 1ull);
+    }
+  }
+  __syncthreads();
+  const int d1 = A.d + 1;
+  for (int i = threadIdx.x; i < (DP + 1) * KP; i += WAVES * 64) {
+    const int j = i / (DP + 1);
+    const int f = i - j * (DP + 1);
+    const double v = tab[(size_t)f * TS + j];
+    if (v != 0.0 && (f < A.d || f == DP) && j < A.k) atomicAdd(A.stats + (size_t)j * d1 + (f == DP ? A.d : f), v);
+  }
+}
+
 #ifdef KM_DIAG  // the fast screen is a diagnostic-build experiment (DESIGN.md "Fast screen")
 // ---------------------------------------------------------------------------
 // Fast screen (k_fused1): ONE fp16 image of -2cs (128 AGPRs instead of 256)
@@ -2217,10 +2699,16 @@ void dump_fused_stamps() {
   }
   unsigned long long tot = 0;
   for (int i = 0; i < 5; ++i) tot += v[i];
-  fprintf(stderr, "[km stamps] total %llu\n", tot);
+  fprintf(stderr, "[km stamps] raw %llu %llu %llu %llu %llu %llu\n", v[0], v[1], v[2], v[3], v[4], v[5]);
   if (tot == 0) return;
-  fprintf(stderr, "[km stamps] split %.3f blocks %.3f merge %.3f queue %.3f sums %.3f (fractions)\n",
-          (double)v[0] / tot, (double)v[1] / tot, (double)v[2] / tot, (double)v[3] / tot, (double)v[4] / tot);
+  if (v[5]) {  // KM_ABLATE=9 (k_fusedp): head / region / tail per wave, kernel cycles, realtime ticks, waves
+    fprintf(stderr, "[km stamps] k_fusedp per wave: head %.0f region %.0f tail %.0f kernel %.0f cycles; "
+                    "clock %.3f GHz\n", (double)v[0] / v[5], (double)v[1] / v[5], (double)v[2] / v[5],
+            (double)v[3] / v[5], v[4] ? (double)v[3] / (double)v[4] * 0.1 : 0.0);
+  } else {
+    fprintf(stderr, "[km stamps] split %.3f blocks %.3f merge %.3f queue %.3f sums %.3f (fractions)\n",
+            (double)v[0] / tot, (double)v[1] / tot, (double)v[2] / tot, (double)v[3] / tot, (double)v[4] / tot);
+  }
   unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z));
 }
@@ -2299,21 +2787,22 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
   FusedArgs a{X, xnorm, g.n, g.k, g.d, seg, ChiF, CloF, cn2s, bnd, xabs, cabs, labels, queue, qcount, stats, gate,
                 C64P, sse};
   const size_t lds = (size_t)g.kp * 4 + (with_stats ? (size_t)(g.dp + 1) * g.kp * 8 : 0);
+  const size_t lds_p = (size_t)g.kp * 4 + (size_t)(g.dp + 1) * (g.kp + 1) * 8;  // k_fusedp: discard column
 #define KM_FUSED_CASE(NS_, NB_)                                                                        \
   case NS_ * 100 + NB_:                                                                                \
     if (with_stats && sse)                                                                             \
       hipLaunchKernelGGL((k_fused<NS_, NB_, true, 0, true, true>), dim3(nbk), dim3(256), lds, s, a);   \
     else if (with_stats && !refine)                                                                    \
-      hipLaunchKernelGGL((k_fused<NS_, NB_, true, 0, false>), dim3(nbk), dim3(256), lds, s, a);        \
+      hipLaunchKernelGGL((k_fusedp<NS_, NB_, false>), dim3(nbk), dim3(256), lds_p, s, a);              \
     else if (with_stats)                                                                               \
-      hipLaunchKernelGGL((k_fused<NS_, NB_, true>), dim3(nbk), dim3(256), lds, s, a);                  \
+      hipLaunchKernelGGL((k_fusedp<NS_, NB_, true>), dim3(nbk), dim3(256), lds_p, s, a);               \
     else                                                                                               \
       hipLaunchKernelGGL((k_fused<NS_, NB_, false>), dim3(nbk), dim3(256), lds, s, a);                 \
     break;
 #ifdef KM_DIAG
   {
     static const int abl = diag_env("KM_ABLATE", 0);
-    if (abl >= 1 && abl <= 8 && ns == 4 && nb == 8 && with_stats) {
+    if (abl >= 1 && abl <= 9 && ns == 4 && nb == 8 && with_stats && !sse) {
       switch (abl) {
         case 1: hipLaunchKernelGGL((k_fused<4, 8, true, 1>), dim3(nbk), dim3(256), lds, s, a); break;
         case 2: hipLaunchKernelGGL((k_fused<4, 8, true, 2>), dim3(nbk), dim3(256), lds, s, a); break;
@@ -2322,6 +2811,7 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
         case 7: hipLaunchKernelGGL((k_fused<4, 8, true, 7>), dim3(nbk), dim3(256), lds, s, a); break;
         case 8: hipLaunchKernelGGL((k_fused<4, 8, true, 8>), dim3(nbk), dim3(256), lds, s, a); break;
         case 6: hipLaunchKernelGGL((k_fused<4, 8, true, 6>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 9: hipLaunchKernelGGL((k_fusedp<4, 8, false, true>), dim3(nbk), dim3(256), lds_p, s, a); break;
         default: hipLaunchKernelGGL((k_fused<4, 8, true, 4>), dim3(nbk), dim3(256), lds, s, a); break;
       }
       return hipGetLastError();
@@ -3064,26 +3554,58 @@ __global__ __launch_bounds__(1024) void k_scan(const uint32_t* __restrict__ cnt,
     }
 }
 
-__global__ __launch_bounds__(256) void k_scatter(const int32_t* __restrict__ labels, int64_t n, int k,
-                                                 uint32_t* __restrict__ cur, uint32_t* __restrict__ perm,
-                                                 int32_t* __restrict__ slab, const int* __restrict__ gate) {
+// Scatter of row ids into label-sorted order.  A workgroup takes a contiguous
+// chunk of SCAT_PER rows and aggregates before touching global memory: each
+// row gets its rank among the chunk's rows of the same label from one LDS
+// counter per label (returning LDS atomics, wave-aggregated by peel_labels),
+// then ONE returning global cursor atomic per (chunk, label present) reserves
+// that label's slots.  Where a few clusters hold most rows (c5_poor: ~3
+// clusters of 50M rows) a per-row or per-wave global atomic serialises every
+// wave of the chip on the same few words at the memory side.
+static constexpr int SCAT_THREADS = 1024, SCAT_ROWS = 8;
+static constexpr int SCAT_PER = SCAT_THREADS * SCAT_ROWS;  // rows per workgroup
+
+__global__ __launch_bounds__(SCAT_THREADS) void k_scatter(const int32_t* __restrict__ labels, int64_t n, int k,
+                                                          uint32_t* __restrict__ cur, uint32_t* __restrict__ perm,
+                                                          int32_t* __restrict__ slab, const int* __restrict__ gate) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
-  // one returning cursor atomic per (wave, hot label) instead of per row
-  // (peel_labels); wave-uniform trip count
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < n; i0 += stride) {
-    const int64_t i = i0 + (threadIdx.x & 63);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);  // [k] chunk counts, then the chunk's base per label
+  for (int i = threadIdx.x; i < k; i += SCAT_THREADS) cnt[i] = 0u;
+  __syncthreads();
+  const int64_t c0 = (int64_t)blockIdx.x * SCAT_PER;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int lab[SCAT_ROWS];
+  uint32_t rnk[SCAT_ROWS];
+  // wave w takes rows c0 + (u * (SCAT_THREADS / 64) + w) * 64 + lane: each
+  // wave-instruction reads 64 consecutive labels
+#pragma unroll
+  for (int u = 0; u < SCAT_ROWS; ++u) {
+    const int64_t i = c0 + ((int64_t)(u * (SCAT_THREADS / 64) + wave) << 6) + lane;
     const int l = i < n ? labels[i] : -1;
     const bool valid = (unsigned)l < (unsigned)k;
     const Peel p = peel_labels<4>(l, valid);
     uint32_t base = 0u;
-    if (p.add) base = atomicAdd(cur + l, p.add);
+    if (p.add) base = atomicAdd(cnt + l, p.add);
     base = (uint32_t)__shfl((int)base, p.leader);
-    if (valid) {
-      const uint32_t pos = base + p.rank;
-      perm[pos] = (uint32_t)i;
-      slab[pos] = l;
-    }
+    lab[u] = valid ? l : -1;
+    rnk[u] = base + p.rank;
+  }
+  __syncthreads();
+  // one cursor atomic per label present in the chunk; the count becomes the
+  // chunk's first slot of that label
+  for (int j = threadIdx.x; j < k; j += SCAT_THREADS) {
+    const uint32_t c = cnt[j];
+    if (c) cnt[j] = atomicAdd(cur + j, c);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < SCAT_ROWS; ++u) {
+    if (lab[u] < 0) continue;
+    const int64_t i = c0 + ((int64_t)(u * (SCAT_THREADS / 64) + wave) << 6) + lane;
+    const uint32_t pos = cnt[lab[u]] + rnk[u];
+    perm[pos] = (uint32_t)i;
+    slab[pos] = lab[u];
   }
 }
 
@@ -3217,10 +3739,11 @@ hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t*
   if (hist_lds > 64 * 1024) return hipErrorInvalidValue;  // k <= 16384
   hipLaunchKernelGGL(k_hist, dim3((unsigned)hb), dim3(1024), hist_lds, s, labels, g.n, g.k, cnt, gate);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, cnt, g.k, off, cur, gate);
-  int64_t sb = (g.n + 255) / 256;
-  if (sb > n_cu * 16) sb = n_cu * 16;
+  const int64_t sb = (g.n + SCAT_PER - 1) / SCAT_PER;
+  if (sb > 0x7fffffff) return hipErrorInvalidValue;
   int32_t* slab = reinterpret_cast<int32_t*>(perm + g.n);
-  hipLaunchKernelGGL(k_scatter, dim3((unsigned)sb), dim3(256), 0, s, labels, g.n, g.k, cur, perm, slab, gate);
+  hipLaunchKernelGGL(k_scatter, dim3((unsigned)sb), dim3(SCAT_THREADS), (size_t)g.k * 4, s, labels, g.n, g.k, cur,
+                     perm, slab, gate);
   hipLaunchKernelGGL(k_put_counts, dim3((g.k + 255) / 256), dim3(256), 0, s, cnt, g.k, g.d, stats, gate);
   // every label is in [0, k) (the assign kernels map non-finite rows to 0),
   // so all n sorted positions are written

@@ -475,7 +475,7 @@ int km_sync(km_ctx* c) {
   KM_HIP(hipSetDevice(c->device));
   KM_HIP(hipStreamSynchronize(c->stream));
 #ifdef KM_DIAG
-  if (km::diag_env("KM_ABLATE", 0) == 7) km::dump_fused_stamps();
+  if (km::diag_env("KM_ABLATE", 0) == 7 || km::diag_env("KM_ABLATE", 0) == 9) km::dump_fused_stamps();
 #endif
   return KM_OK;
 }
