@@ -147,7 +147,7 @@ int km_update(km_ctx* ctx, km_status* st, int64_t* counts);
  * kmeans_spark.py:191-204 onto the device inside batches: after an update
  * with empty clusters, takeSample(False, n_empty, empty_seed) runs there
  * (PySpark's fraction, per-partition Bernoulli passes with CPython's MT19937,
- * retry, shuffle), its rows replace the empty clusters and their shifts enter
+ * shuffle; one pass, no retry), its rows replace the empty clusters and their shifts enter
  * max_shift, without stopping the batch (km_status.repaired = 1).  Otherwise
  * (or if a pass overflows its slots or comes back short: the device does not
  * retry PySpark's resampling loop) empty clusters stop the batch and the

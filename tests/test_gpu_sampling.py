@@ -34,6 +34,20 @@ def test_device_bernoulli_equals_host(engine, sizes, fraction, seed):
     np.testing.assert_array_equal(got, want)
 
 
+def test_device_bernoulli_equals_cpython_literals(engine):
+    # the literal picks of CPython's random module (tests/test_host.py
+    # CPYTHON_PICKS): the device MT19937 against CPython itself, not only
+    # against the host restatement
+    from test_host import CPYTHON_PICKS
+    for sizes, fraction, seed, want in CPYTHON_PICKS:
+        bases = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+        mine = [p for p in range(len(sizes)) if sizes[p] > 0]
+        got = engine.bernoulli(np.array([seed ^ p for p in mine], dtype=np.uint64),
+                               np.array([sizes[p] for p in mine]), bases[mine], fraction)
+        assert got is not None
+        assert got.tolist() == want
+
+
 def test_take_sample_with_device_pass(engine):
     from kmeans_amd import sampling
     sizes = [300_000, 200_001, 0, 150_000]

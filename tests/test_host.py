@@ -121,6 +121,45 @@ def test_device_pass_keys_for_negative_and_huge_seeds():
     assert not calls or all(max(c) < 2 ** 64 for c in calls)
 
 
+# Literal outputs of CPython's own random module (3.10, MT19937 +
+# init_by_array seeding + getrandbits rejection in randint), written down
+# once: they pin the samplers to CPython independently of the oracle's
+# restatement, so a drift shared by sampling.py and the oracle is caught.
+CPYTHON_PICKS = [
+    ([1000, 313, 1, 0, 700], 0.01, 42,
+     [10, 115, 260, 281, 288, 359, 385, 418, 472, 675, 873, 1142, 1229, 1241, 1361, 1425, 1490, 1757, 1791,
+      2013]),
+    ([624, 623, 625], 0.02, 2 ** 40 + 7,
+     [118, 151, 165, 201, 243, 309, 321, 493, 545, 546, 586, 601, 611, 735, 748, 765, 849, 881, 925, 1071,
+      1113, 1123, 1148, 1180, 1235, 1312, 1340, 1365, 1401, 1444, 1526, 1563, 1603, 1674, 1678, 1708, 1779]),
+]
+CPYTHON_TAKESAMPLE = [
+    ([250, 250, 250, 250], 6, 42, [646, 533, 479, 991, 705, 319]),
+    ([40000, 40000], 12, 6, [35818, 44499, 38713, 65870, 12098, 30608, 29487, 57706, 18963, 59044, 14022, 7334]),
+    ([333, 333, 334], 5, 1700000000, [210, 862, 94, 524, 953]),
+]
+
+
+@pytest.mark.parametrize("sizes,fraction,seed,want", CPYTHON_PICKS)
+def test_bernoulli_pass_pinned_to_cpython_literals(sizes, fraction, seed, want):
+    import random
+    from kmeans_amd import sampling
+    r = random.Random(12345)
+    assert [r.random() for _ in range(3)] == [0.41661987254534116, 0.010169169457068361, 0.8252065092537432]
+    assert sampling._bernoulli_pass_py(sizes, fraction, seed) == want
+    bases = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    got = np.concatenate([sampling._partition_picks(p, int(bases[p]), sizes[p], fraction, seed)
+                          for p in range(len(sizes)) if sizes[p] > 0])
+    assert got.tolist() == want
+
+
+@pytest.mark.parametrize("sizes,num,seed,want", CPYTHON_TAKESAMPLE)
+def test_take_sample_pinned_to_cpython_literals(sizes, num, seed, want):
+    from kmeans_amd import sampling
+    assert sampling.take_sample(sizes, num, seed) == want
+    assert orc.take_sample_indices(sizes, num, seed) == want
+
+
 def test_vectorised_sampler_equals_python_sampler():
     from kmeans_amd import sampling
     sizes = [70001, 30000]
