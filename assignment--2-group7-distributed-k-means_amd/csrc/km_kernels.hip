@@ -1734,7 +1734,11 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
 //     other of two ping-pong B-operand sets.
 // What stays between blocks is the last block's keys and the merge / bound /
 // label / queue of tile t.
+// Diagnostic build only (KM_ABLATE=10; 9 with phase stamps): parity-green, but
+// no faster than k_fused in A/B/A runs on one box (11.2 ms both, DESIGN.md
+// section 4) -- the c3 screen is at its power floor, not schedule-bound.
 // ---------------------------------------------------------------------------
+#ifdef KM_DIAG
 // STAMP (diagnostic build, KM_ABLATE=9): s_memtime phase stamps per tile
 // (head = loads + block 0, region = blocks 1 .. NB-1, tail = last keys +
 // merge + queue), the wave's whole-kernel cycles and s_memrealtime ticks
@@ -2197,6 +2201,7 @@ __global__ __launch_bounds__(256, 1) void k_fusedp(FusedArgs A) {
     if (v != 0.0 && (f < A.d || f == DP) && j < A.k) atomicAdd(A.stats + (size_t)j * d1 + (f == DP ? A.d : f), v);
   }
 }
+#endif  // KM_DIAG (k_fusedp)
 
 #ifdef KM_DIAG  // the fast screen is a diagnostic-build experiment (DESIGN.md "Fast screen")
 // ---------------------------------------------------------------------------
@@ -2787,22 +2792,24 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
   FusedArgs a{X, xnorm, g.n, g.k, g.d, seg, ChiF, CloF, cn2s, bnd, xabs, cabs, labels, queue, qcount, stats, gate,
                 C64P, sse};
   const size_t lds = (size_t)g.kp * 4 + (with_stats ? (size_t)(g.dp + 1) * g.kp * 8 : 0);
+#ifdef KM_DIAG
   const size_t lds_p = (size_t)g.kp * 4 + (size_t)(g.dp + 1) * (g.kp + 1) * 8;  // k_fusedp: discard column
+#endif
 #define KM_FUSED_CASE(NS_, NB_)                                                                        \
   case NS_ * 100 + NB_:                                                                                \
     if (with_stats && sse)                                                                             \
       hipLaunchKernelGGL((k_fused<NS_, NB_, true, 0, true, true>), dim3(nbk), dim3(256), lds, s, a);   \
     else if (with_stats && !refine)                                                                    \
-      hipLaunchKernelGGL((k_fusedp<NS_, NB_, false>), dim3(nbk), dim3(256), lds_p, s, a);              \
+      hipLaunchKernelGGL((k_fused<NS_, NB_, true, 0, false>), dim3(nbk), dim3(256), lds, s, a);        \
     else if (with_stats)                                                                               \
-      hipLaunchKernelGGL((k_fusedp<NS_, NB_, true>), dim3(nbk), dim3(256), lds_p, s, a);               \
+      hipLaunchKernelGGL((k_fused<NS_, NB_, true>), dim3(nbk), dim3(256), lds, s, a);                  \
     else                                                                                               \
       hipLaunchKernelGGL((k_fused<NS_, NB_, false>), dim3(nbk), dim3(256), lds, s, a);                 \
     break;
 #ifdef KM_DIAG
   {
     static const int abl = diag_env("KM_ABLATE", 0);
-    if (abl >= 1 && abl <= 9 && ns == 4 && nb == 8 && with_stats && !sse) {
+    if (abl >= 1 && abl <= 10 && ns == 4 && nb == 8 && with_stats && !sse) {
       switch (abl) {
         case 1: hipLaunchKernelGGL((k_fused<4, 8, true, 1>), dim3(nbk), dim3(256), lds, s, a); break;
         case 2: hipLaunchKernelGGL((k_fused<4, 8, true, 2>), dim3(nbk), dim3(256), lds, s, a); break;
@@ -2812,6 +2819,7 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
         case 8: hipLaunchKernelGGL((k_fused<4, 8, true, 8>), dim3(nbk), dim3(256), lds, s, a); break;
         case 6: hipLaunchKernelGGL((k_fused<4, 8, true, 6>), dim3(nbk), dim3(256), lds, s, a); break;
         case 9: hipLaunchKernelGGL((k_fusedp<4, 8, false, true>), dim3(nbk), dim3(256), lds_p, s, a); break;
+        case 10: hipLaunchKernelGGL((k_fusedp<4, 8, false>), dim3(nbk), dim3(256), lds_p, s, a); break;
         default: hipLaunchKernelGGL((k_fused<4, 8, true, 4>), dim3(nbk), dim3(256), lds, s, a); break;
       }
       return hipGetLastError();
