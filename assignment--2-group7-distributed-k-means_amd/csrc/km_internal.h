@@ -14,8 +14,9 @@ namespace km {
 struct QEntry {
   uint32_t row;   // local row
   uint32_t i1;    // best screened centroid
-  uint32_t i2;    // second best screened centroid
-  uint32_t kind;  // 1 = re-rank {i1,i2}, 2 = full exact scan, 3 = scan of the chain j & 7 == i1 & 7
+  uint32_t i2;    // second best screened centroid (kind 4: record of the candidate pool)
+  uint32_t kind;  // 1 = re-rank {i1,i2}, 2 = full exact scan, 3 = scan of the chain j & 7 == i1 & 7,
+                  // 4 = re-rank of a candidate list (k_assign_mfma)
 };
 
 // Per-iteration status produced on device by k_finalize (kmeans_spark.py:176-313
@@ -73,10 +74,15 @@ hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C
 bool small_path_ok(const Geometry& g);
 // MFMA path: fp16x3 screening on v_mfma_f32_32x32x16_f16, top-3 keys,
 // ambiguous points queued for the exact resolvers.
+// cand / cand_ctr / cand_cap: pool of candidate lists (kind-4 queue entries,
+// cand_rec_words() words each; the counter is zeroed by the launch); nullptr:
+// every kind-2 point is left to the full scan
 hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16* Chi, const _Float16* Clo,
                               const float* cn2s, const float* cmax, const float* xabs, const float* cabs,
                               int32_t* labels, QEntry* queue, uint32_t* qcount, int n_cu, QLayout* ql,
-                              const int* gate, hipStream_t s);
+                              const int* gate, hipStream_t s, uint32_t* cand = nullptr, uint32_t* cand_ctr = nullptr,
+                              uint32_t cand_cap = 0);
+int cand_rec_words();
 // queue capacity (entries) and per-wave counter words needed for n rows
 size_t queue_capacity(int64_t n, int n_cu);
 size_t qcount_words(int n_cu);
@@ -84,7 +90,8 @@ bool mfma_path_ok(const Geometry& g);
 // stats != nullptr: also add the resolved points' rows to the partial sums
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
-                          double* stats, int n_cu, const int* gate, hipStream_t s, double* sse = nullptr);
+                          double* stats, int n_cu, const int* gate, hipStream_t s, double* sse = nullptr,
+                          const uint32_t* cand = nullptr, uint32_t cand_cap = 0);
 // Fused assign + partial sums (kp*dp <= 16384 class): fp16 hi image in VGPRs,
 // lo image + float64 sum table in LDS; decided points summed here, queued
 // points (and their counts) by launch_resolve(stats).

@@ -500,6 +500,9 @@ __device__ __forceinline__ void top3p_insert(float& k1, float& k2, float& k3, ui
   k3 = n3;
 }
 
+static constexpr int CAND_REC = 16;  // candidate record: count + up to 15 centroid indices, ascending
+int cand_rec_words() { return CAND_REC; }
+
 template <int NS, int WAVES>
 constexpr int mfma_min_waves() {
   return WAVES == 4 ? 1 : (WAVES == 12 ? 3 : (NS <= 4 ? 4 : 2));
@@ -520,6 +523,9 @@ struct MfmaArgs {
   QEntry* queue;
   uint32_t* qcount;
   const int* gate;  // nonzero: a stopped batch, the launch is a no-op
+  uint32_t* cand;      // candidate pool (kind-4 entries): CAND_REC words per record, nullptr: off
+  uint32_t* cand_ctr;  // records taken this launch (zeroed before it)
+  uint32_t cand_cap;   // records
 };
 
 // LDS image of a centroid chunk: for block b (32 centroids) and K-step t the
@@ -844,14 +850,87 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
       else if (kind == 2u && !same_chain && kb.lower(k3) > u1)
         kind = 1u;  // the rest (key >= k3) is worse than i1: the answer is i1 or i2
     }
+    // Candidate lists (kind 4) instead of full scans.  A kind-2 point has more
+    // than two keys within the bound of k1, but each chain keeps its best keys
+    // with their indices (top 3: two indexed, T2: one) and knows that every key
+    // it dropped is >= its guard (third, T2: second).  When no chain's guard is
+    // within the bound, every centroid that can be the argmin is one of the kept
+    // keys within it: those few are re-ranked in float64 (k_rerank2) instead
+    // of a scan over all k.  Exactness as for kind 1: the true argmin j* has
+    // S_j* <= S_p1, so its key passes the same two tests that exclude the others.
+    if (A.cand != nullptr && __ballot(kind == 2u) != 0ull) {
+      uint32_t cj[8];  // this lane half's kept candidates (0xffffffff: none)
+      bool over = !(k1 == k1) || !(fabsf(k1) < 3.0e38f);
+      if (kind == 2u) {
+        const KeyBounds kb = key_bounds(xn, *A.xabs * s, DP, rho);
+        const float u1 = kb.upper(k1);
+        auto maybe = [&](float v) {  // v's centroid may be the argmin (NaN: yes)
+          return !(v - k1 > 2.0f * B0 + rho * (fabsf(k1) + fabsf(v))) && !(kb.lower(v) > u1);
+        };
+        auto idx = [&](float v, int c) { return ((__float_as_uint(v) & maskq) << 2) | (uint32_t)c; };
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float g = T2 ? a2[c] : a3[c];
+          over |= maybe(g);
+          cj[2 * c] = maybe(a1[c]) ? idx(a1[c], c) : 0xffffffffu;
+          cj[2 * c + 1] = (!T2 && maybe(a2[c])) ? idx(a2[c], c) : 0xffffffffu;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) cj[c] = 0xffffffffu;
+      }
+      // the other lane half's chains (same point)
+      uint32_t co[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) co[c] = __shfl_xor(cj[c], 32);
+      over |= __shfl_xor((int)over, 32) != 0;
+      int nc = 0;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        nc += cj[c] < (uint32_t)A.k;
+        nc += co[c] < (uint32_t)A.k;
+      }
+      const bool want = h == 0 && valid && kind == 2u && !over && nc >= 1 && nc < CAND_REC;
+      const uint64_t m4 = __ballot(want);
+      if (m4) {
+        const int leader = __ffsll((unsigned long long)m4) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(A.cand_ctr, (uint32_t)__popcll(m4));
+        base = __shfl(base, leader);
+        const uint32_t slot = base + (uint32_t)__popcll(m4 & ((1ull << lane) - 1ull));
+        if (want && slot < A.cand_cap) {
+          // ascending index order (np.argmin's tie-break in k_rerank2)
+          uint32_t v[16];
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            v[c] = cj[c] < (uint32_t)A.k ? cj[c] : 0xffffffffu;
+            v[8 + c] = co[c] < (uint32_t)A.k ? co[c] : 0xffffffffu;
+          }
+#pragma unroll
+          for (int i = 1; i < 16; ++i)
+#pragma unroll
+            for (int j2 = i; j2 > 0; --j2) {
+              const uint32_t lo = min(v[j2 - 1], v[j2]), hi = max(v[j2 - 1], v[j2]);
+              v[j2 - 1] = lo;
+              v[j2] = hi;
+            }
+          uint32_t* rec = A.cand + (size_t)slot * CAND_REC;
+          rec[0] = (uint32_t)nc;
+#pragma unroll
+          for (int i = 0; i < CAND_REC - 1; ++i) rec[1 + i] = v[i];
+          kind = 4u;
+          p2 = slot;
+        }
+      }
+    }
     const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
     if (h == 0 && valid) A.labels[row] = lab;
     const bool enq = (h == 0) && valid && (kind != 0);
     const uint64_t m = __ballot(enq);
     if (m) {
-      // re-rank entries fill the wave's segment from the front, full scans
-      // from the back (resolved by different kernels)
-      const uint64_t m1 = __ballot(enq && kind == 1);
+      // re-rank and candidate-list entries fill the wave's segment from the
+      // front, full scans from the back (resolved by different kernels)
+      const uint64_t m1 = __ballot(enq && (kind == 1 || kind == 4));
       const uint64_t m2 = m & ~m1;
       const uint64_t below = (1ull << lane) - 1ull;
       if (enq) {
@@ -860,8 +939,8 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
         q.i1 = p1;
         q.i2 = p2;
         q.kind = kind;
-        const uint32_t pos = (kind == 1) ? qn + (uint32_t)__popcll(m1 & below)
-                                         : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
+        const uint32_t pos = (kind == 1 || kind == 4) ? qn + (uint32_t)__popcll(m1 & below)
+                                                      : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
         wq[pos] = q;
       }
       qn += (uint32_t)__popcll(m1);
@@ -1065,8 +1144,8 @@ __global__ __launch_bounds__(256, 1) void k_assign_wide(MfmaArgs A, int dp) {
         q.i1 = p1;
         q.i2 = p2;
         q.kind = kind;
-        const uint32_t pos = (kind == 1) ? qn + (uint32_t)__popcll(m1 & below)
-                                         : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
+        const uint32_t pos = (kind == 1 || kind == 4) ? qn + (uint32_t)__popcll(m1 & below)
+                                                      : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
         wq[pos] = q;
       }
       qn += (uint32_t)__popcll(m1);
@@ -1156,7 +1235,8 @@ static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, con
 hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16* Chi, const _Float16* Clo,
                               const float* cn2s, const float* cmax, const float* xabs, const float* cabs,
                               int32_t* labels, QEntry* queue, uint32_t* qcount, int n_cu, QLayout* ql,
-                              const int* gate, hipStream_t s) {
+                              const int* gate, hipStream_t s, uint32_t* cand, uint32_t* cand_ctr,
+                              uint32_t cand_cap) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
@@ -1166,7 +1246,8 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
     const uint32_t seg = (uint32_t)(((nwt + nb - 1) / nb) * 32);
     ql->seg = seg;
     ql->nwaves = (uint32_t)(nb * 4);
-    MfmaArgs a{X, g.n, g.k, g.kp, WIDE_KC, seg, Chi, Clo, cn2s, cmax, xabs, cabs, labels, queue, qcount, gate};
+    MfmaArgs a{X, g.n, g.k, g.kp, WIDE_KC, seg, Chi, Clo, cn2s, cmax, xabs, cabs, labels, queue, qcount, gate,
+               nullptr, nullptr, 0};
     const size_t lds = 2 * (size_t)WIDE_KC * WIDE_FW * 2 + (size_t)WIDE_KC * 4;
     hipLaunchKernelGGL(k_assign_wide, dim3(nb), dim3(256), lds, s, a, g.dp);
     return hipGetLastError();
@@ -1188,7 +1269,13 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
   const uint32_t seg = (uint32_t)(((nwt + nb - 1) / nb) * 32);
   ql->seg = seg;
   ql->nwaves = (uint32_t)(nb * waves);
-  MfmaArgs a{X, g.n, g.k, g.kp, KC, seg, Chi, Clo, cn2s, cmax, xabs, cabs, labels, queue, qcount, gate};
+  static const int use_cand = diag_env("KM_CAND", 1);  // candidate lists instead of full scans
+  if (cand != nullptr && use_cand) {
+    const hipError_t e = hipMemsetAsync(cand_ctr, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+  }
+  MfmaArgs a{X, g.n, g.k, g.kp, KC, seg, Chi, Clo, cn2s, cmax, xabs, cabs, labels, queue, qcount, gate,
+             use_cand ? cand : nullptr, cand_ctr, cand_cap};
   switch (g.dp / 16) {
     case 1: launch_mfma_ns<1>(waves, nb, lds, s, a); break;
     case 2: launch_mfma_ns<2>(waves, nb, lds, s, a); break;
@@ -2932,7 +3019,8 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
                                                   const double* __restrict__ C64, const QEntry* __restrict__ queue,
                                                   const uint32_t* __restrict__ qcount, QLayout ql,
                                                   int32_t* __restrict__ labels, double* __restrict__ stats,
-                                                  int tab_kp, double* __restrict__ sse, const int* __restrict__ gate) {
+                                                  int tab_kp, double* __restrict__ sse, const int* __restrict__ gate,
+                                                  const uint32_t* __restrict__ cand, uint32_t cand_cap) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* tab = reinterpret_cast<double*>(smem);
@@ -2955,22 +3043,51 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
       const uint32_t sg = find_segment(pre, ql.nwaves, g);
       q = queue[(size_t)sg * ql.seg + (g - pre[sg])];
     }
-    const bool ok = have && q.i1 < (uint32_t)k && q.i2 < (uint32_t)k;
+    // kind 4: a candidate list (k_assign_mfma), count + ascending indices
+    const uint32_t* rec = (have && q.kind == 4u && cand != nullptr && q.i2 < cand_cap)
+                              ? cand + (size_t)q.i2 * CAND_REC : nullptr;
+    const int nc = rec ? (int)min(rec[0], (uint32_t)(CAND_REC - 1)) : 0;
+    const bool ok = have && (rec ? (nc >= 1 && rec[nc] < (uint32_t)k)
+                                 : (q.kind != 4u && q.i1 < (uint32_t)k && q.i2 < (uint32_t)k));
     const float* __restrict__ x = X + (size_t)q.row * dp;
-    const int a = ok ? (int)min(q.i1, q.i2) : 0, bb = ok ? (int)max(q.i1, q.i2) : 0;
-    const double* __restrict__ ca = C64 + (size_t)a * d;
-    const double* __restrict__ cb = C64 + (size_t)bb * d;
-    double sa, sb;
-    auto sq2 = [&](int f, double& ta, double& tb) {
-      const float xf = x[f];
-      ta = np_sq(ca[f], xf);
-      tb = np_sq(cb[f], xf);
-    };
-    if constexpr (WIDE)
-      np_pw8<5>(sq2, 0, d, u, sa, sb);  // d <= 2048
-    else
-      np_pw8<2>(sq2, 0, d, u, sa, sb);
-    int lab = np_pick_second(sqrt(sa), sqrt(sb)) ? bb : a;
+    int lab = 0;
+    double mnorm = 0.0;  // the chosen centroid's norm (SSE)
+    // np.argmin over ascending candidates, two norms per pass (NumPy's
+    // pairwise order, 8 lanes per entry); kind 1 is the pass over {i1, i2}
+    const int npass = rec ? (ok ? (nc + 1) / 2 : 0) : 1;
+    int bi = -1;
+    for (int t = 0; t < npass; ++t) {
+      int a, bb;
+      if (rec) {
+        a = (int)rec[1 + 2 * t];
+        bb = 2 * t + 1 < nc ? (int)rec[2 + 2 * t] : a;
+      } else {
+        a = ok ? (int)min(q.i1, q.i2) : 0;
+        bb = ok ? (int)max(q.i1, q.i2) : 0;
+      }
+      const double* __restrict__ ca = C64 + (size_t)a * d;
+      const double* __restrict__ cb = C64 + (size_t)bb * d;
+      double sa, sb;
+      auto sq2 = [&](int f, double& ta, double& tb) {
+        const float xf = x[f];
+        ta = np_sq(ca[f], xf);
+        tb = np_sq(cb[f], xf);
+      };
+      if constexpr (WIDE)
+        np_pw8<5>(sq2, 0, d, u, sa, sb);  // d <= 2048
+      else
+        np_pw8<2>(sq2, 0, d, u, sa, sb);
+      const double va = sqrt(sa), vb = sqrt(sb);
+      if (np_better(va, mnorm, bi >= 0)) {
+        mnorm = va;
+        bi = a;
+      }
+      if (bb != a && np_better(vb, mnorm, true)) {
+        mnorm = vb;
+        bi = bb;
+      }
+    }
+    lab = bi < 0 ? 0 : bi;
     if (!have) continue;
     double rsq_bad = 0.0;
     if (!ok && u == 0) {
@@ -2991,7 +3108,7 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
     // SSE (fused path): min_distance ** 2 with the chosen centroid's norm in
     // NumPy's order (kmeans_spark.py:231-233)
     if (sse && u == 0) {
-      const double mn = ok ? sqrt(lab == bb ? sb : sa) : rsq_bad;
+      const double mn = ok ? mnorm : rsq_bad;
       ss_acc += mn * mn;
     }
     if (stats) {
@@ -3252,7 +3369,8 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
 
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
-                          double* stats, int n_cu, const int* gate, hipStream_t s, double* sse) {
+                          double* stats, int n_cu, const int* gate, hipStream_t s, double* sse,
+                          const uint32_t* cand, uint32_t cand_cap) {
   if (g.n == 0 || ql.nwaves == 0) return hipSuccess;
   constexpr size_t LDS_MAX = 160 * 1024;
   const size_t pre_bytes = ((size_t)ql.nwaves + 1) * 4;
@@ -3286,10 +3404,10 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   const int tab_kp = (stats && tab_bytes + pres <= LDS_MAX) ? g.kp : 0;
   if (g.d > 256)
     hipLaunchKernelGGL(k_rerank2<true>, dim3(n_cu), dim3(512), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
-                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate);
+                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap);
   else
     hipLaunchKernelGGL(k_rerank2<false>, dim3(n_cu), dim3(1024), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
-                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate);
+                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap);
   return hipGetLastError();
 }
 

@@ -98,6 +98,9 @@ struct km_ctx {
   int32_t* labels = nullptr;
   km::QEntry* queue = nullptr;
   uint32_t* qcount = nullptr;
+  uint32_t* cand = nullptr;      // candidate-list pool of the MFMA screen (kind-4 entries)
+  uint32_t* cand_ctr = nullptr;  // its per-launch record counter
+  uint32_t cand_cap = 0;         // records
   km::QLayout ql{0, 0};
   double* moments = nullptr;  // d+1 scratch
   bool want_sse = false;      // km_set_sse: SSE residuals in km_assign_stats
@@ -248,6 +251,9 @@ void free_data(km_ctx* c) {
   dfree(c->labels);
   dfree(c->queue);
   dfree(c->qcount);
+  dfree(c->cand);
+  dfree(c->cand_ctr);
+  c->cand_cap = 0;
   dfree(c->moments);
   dfree(c->xabs);
   dfree(c->xnorm);
@@ -360,15 +366,25 @@ int run_assign(km_ctx* c, bool with_stats) {
     }
     return KM_OK;  // counts are part of the fused and resolver statistics
   }
+  if (!c->cand && g.dp <= 256) {
+    // candidate lists of the points the screen cannot settle between its top
+    // two (kind 4): up to 4M records of 64 B; a full pool leaves the rest to
+    // the full scans
+    const int64_t cap = std::min<int64_t>(std::max<int64_t>(g.n, 1024), (int64_t)1 << 22);
+    KM_HIP(hipMalloc(&c->cand, sizeof(uint32_t) * km::cand_rec_words() * (size_t)cap));
+    KM_HIP(hipMalloc(&c->cand_ctr, sizeof(uint32_t)));
+    c->cand_cap = (uint32_t)cap;
+  }
   {
     ProfScope ps(c, KM_K_ASSIGN);
     KM_HIP(km::launch_assign_mfma(c->X, g, c->Chi, c->Clo, c->cn2s, c->cmax, c->xabs, c->cabs, c->labels, c->queue,
-                                  c->qcount, c->n_cu, &c->ql, c->gate, c->stream));
+                                  c->qcount, c->n_cu, &c->ql, c->gate, c->stream, c->cand, c->cand_ctr,
+                                  c->cand_cap));
   }
   {
     ProfScope ps(c, KM_K_RESOLVE);
     KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels, nullptr, c->n_cu,
-                              c->gate, c->stream));
+                              c->gate, c->stream, nullptr, c->cand, c->cand_cap));
   }
   if (with_stats) {
     ProfScope ps(c, KM_K_STATS);

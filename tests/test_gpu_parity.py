@@ -292,6 +292,38 @@ def test_near_ties_one_ulp_apart_vs_oracle(n, d, nb, off):
     np.testing.assert_array_equal(labels, lab_ref)
 
 
+@pytest.mark.parametrize("n,d,nb,copies,top3", [
+    (8000, 100, 100, 3, True),    # dp 128 (top-3 chains), kp 320: copies on other and on the same chain
+    (8000, 64, 81, 4, True),      # four ulp-copies on four chains (kp 384, unfused)
+    (8000, 64, 80, 4, False),     # four copies on ONE chain (80 = 0 mod 8): the guard overflows -> full scan
+    (6000, 32, 100, 3, False),    # top-2 chains (d <= 32): two copies on one chain overflow -> full scan
+    (4000, 128, 601, 3, True),    # k = 1803: chunked centroid images (c5 class)
+])
+def test_candidate_lists_multi_ties_vs_oracle(n, d, nb, copies, top3):
+    # three or four centroids one float64 ulp apart: no pair certificate (kind
+    # 2).  The MFMA screen lists the chains' kept keys within the bound
+    # (kind 4) when no chain's guard key is within it, and k_rerank2 resolves
+    # the list in float64 -- labels must be np.argmin over np.linalg.norm bit
+    # for bit, and the candidate lists must replace most full scans
+    X = _blobs(n, d, 32, 41 + d)
+    base = X[np.random.default_rng(d + nb).choice(n, nb, replace=False)]
+    cs = [base]
+    for _ in range(copies - 1):
+        cs.append(np.nextafter(cs[-1], np.inf))
+    C0 = np.concatenate(cs)
+    km = _one_step(X, C0, iters=1)
+    lab_ref = orc.assign(X, C0)[0]
+    np.testing.assert_array_equal(km._runner.engine.labels(), lab_ref)
+    # (the copies that win no point are empty clusters, replaced by a
+    # time-seeded takeSample: only the labels and the SSE are deterministic)
+    ref = orc.lloyd_fit(X, len(C0), 1, 1e-12, 0, True, 1, init_centroids=C0)
+    np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)
+    last = km._runner.last
+    assert last["q_rerank"] + last["q_full"] > n // 2          # nearly every point is a multi-tie
+    if top3:
+        assert last["q_full"] < n // 4, last                 # most go to candidate lists, not full scans
+
+
 @pytest.mark.parametrize("n,d,nb", [(3000, 300, 30), (1500, 784, 16), (1200, 2000, 8)])
 def test_wide_rows_triple_ties_full_scan_vs_oracle(n, d, nb):
     # three centroids one float64 ulp apart: no re-rank certificate, so the
