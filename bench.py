@@ -211,9 +211,10 @@ def main():
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
-            if tj.get("config") == args.config and tj.get("kernel") == dom:
+            te = tj.get(args.config) if "config" not in tj else (tj if tj["config"] == args.config else None)
+            if te is not None and te.get("kernel", "assign") == dom:
                 # measured on one GPU holding all N rows; a rank's launch covers n_local
-                traffic = tj.get("bytes_per_launch") * n_local / N
+                traffic = te.get("bytes_per_launch") * n_local / N
         except Exception:
             traffic = None
     if info["path"] == 2 and dom == "assign" and screen in (2, 3):
