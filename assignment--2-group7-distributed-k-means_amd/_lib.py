@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(HERE, "libkmeans_amd.so")
 ROOT = os.path.dirname(HERE)
 HEADER = os.path.join(ROOT, "include", "kmeans_amd.h")
 
-KM_ABI_VERSION = 3
+KM_ABI_VERSION = 4
 KM_OK = 0
 KM_EMPTY = 1
 
@@ -77,6 +77,10 @@ SIGNATURES = {
     "km_batch_begin": [_P],
     "km_update_async": [_P, _D, _I64],
     "km_set_layout": [_P, _PI64, _I32, _I64, _I32],
+    "km_repair_state": [_P, _PI32, _PI32],
+    "km_repair_buffer": [_P, ctypes.POINTER(_P), _PI64],
+    "km_bind_repair_buffer": [_P, _P],
+    "km_repair_apply_async": [_P],
     "km_batch_end": [_P, ctypes.POINTER(KmStatus), _PI64, _PI32],
     "km_replace_rows": [_P, _PI32, _PD, _I32],
     "km_commit": [_P],

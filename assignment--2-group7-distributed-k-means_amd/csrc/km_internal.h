@@ -155,6 +155,17 @@ hipError_t launch_repair(int* gate, const int64_t* counts, const Geometry& g, in
                          uint64_t seed, int32_t* empty, int32_t* pcounts, int64_t* picks, int64_t* samples, int cp,
                          const int64_t* sizes, const int64_t* bases, int nparts, const float* X, int64_t row0,
                          const double* C_old, double* C_new, DevStatus* st, double tol, hipStream_t s);
+// the same repair with the rows spread over ranks: pick writes the picked rows
+// this context holds into rows[num][d] (zeros for the others) and pending =
+// num; the caller sum-all-reduces rows; apply puts them in place
+hipError_t launch_repair_pick(int* gate, const int64_t* counts, const Geometry& g, int64_t total,
+                              double neg_log_delta, uint64_t seed, int32_t* empty, int32_t* pcounts, int64_t* picks,
+                              int64_t* samples, int cp, const int64_t* sizes, const int64_t* bases, int nparts,
+                              const float* X, int64_t row0, DevStatus* st, double* rows, int32_t* pending,
+                              hipStream_t s);
+hipError_t launch_repair_apply(int* gate, const Geometry& g, const int32_t* empty, const double* C_old,
+                               double* C_new, DevStatus* st, double tol, const double* rows, const int32_t* pending,
+                               hipStream_t s);
 // takeSample's Bernoulli pass, one wave per partition (km_sample.hip)
 hipError_t launch_bernoulli(const uint64_t* seeds, const int64_t* sizes, const int64_t* bases, int nparts,
                             double fraction, int64_t* out, int cp, int32_t* counts, hipStream_t s);

@@ -158,6 +158,13 @@ struct km_ctx {
   int32_t* rep_pcounts = nullptr; // [nparts]
   int64_t* rep_picks = nullptr;   // [nparts][cp]
   int64_t* rep_samples = nullptr; // [nparts * cp]
+  int rep_mode = 0;               // km_set_layout: 1 every row here, 2 rows spread over ranks
+  double* rep_rows = nullptr;     // mode 2: replacement rows [k][d], all-reduced by the caller
+  double* rep_rows_own = nullptr; // the context's own buffer (unless km_bind_repair_buffer)
+  int32_t* rep_pending = nullptr; // mode 2: rows picked by the last k_rep_pick (device word)
+  bool rep_wait = false;          // mode 2: km_update_async left the iteration to km_repair_apply_async
+  double rep_tol = 0.0;
+  bool rep_fold = false;
   // staging
   float* pinned = nullptr;      // two staging halves of pinned_floats each
   size_t pinned_floats = 0;
@@ -299,6 +306,9 @@ void free_repair(km_ctx* c) {
   dfree(c->rep_pcounts);
   dfree(c->rep_picks);
   dfree(c->rep_samples);
+  dfree(c->rep_rows_own);
+  dfree(c->rep_pending);
+  c->rep_rows = nullptr;
   c->rep_cp = 0;
   c->rep_k = 0;
 }
@@ -326,6 +336,12 @@ int ensure_repair(km_ctx* c) {
   KM_HIP(hipMemsetAsync(c->rep_pcounts, 0, sizeof(int32_t) * c->rep_nparts, c->stream));
   KM_HIP(hipMalloc(&c->rep_picks, sizeof(int64_t) * slots));
   KM_HIP(hipMalloc(&c->rep_samples, sizeof(int64_t) * slots));
+  KM_HIP(hipMalloc(&c->rep_pending, sizeof(int32_t)));
+  KM_HIP(hipMemsetAsync(c->rep_pending, 0, sizeof(int32_t), c->stream));
+  if (c->rep_mode == 2) {
+    KM_HIP(hipMalloc(&c->rep_rows_own, sizeof(double) * (size_t)c->g.k * std::max(1, c->g.d)));
+    c->rep_rows = c->rep_rows_own;
+  }
   c->rep_k = c->g.k;
   return KM_OK;
 }
@@ -794,10 +810,15 @@ int km_set_layout(km_ctx* c, const int64_t* sizes, int32_t nparts, int64_t row0,
     c->rep_total += sizes[i];
     c->rep_maxpart = std::max(c->rep_maxpart, sizes[i]);
   }
+  KM_REQUIRE(device_repair >= 0 && device_repair <= 2, KM_ERR_ARG, "km_set_layout: device_repair must be 0, 1 or 2");
+  c->rep_mode = device_repair;
   if (device_repair) {
-    // every replacement row must be resident here (one rank holding all rows)
-    KM_REQUIRE(row0 == 0 && c->rep_total == c->g.n && nparts > 0, KM_ERR_ARG,
-               "km_set_layout: device repair needs every row of the dataset on this context");
+    // mode 1: every replacement row is resident here (one rank holding all
+    // rows); mode 2: this context holds rows [row0, row0 + n) of the dataset
+    KM_REQUIRE(device_repair == 2 || (row0 == 0 && c->rep_total == c->g.n), KM_ERR_ARG,
+               "km_set_layout: device repair mode 1 needs every row of the dataset on this context");
+    KM_REQUIRE(nparts > 0 && row0 >= 0 && row0 + c->g.n <= c->rep_total, KM_ERR_ARG,
+               "km_set_layout: this context's rows lie outside the layout");
     KM_HIP(hipMalloc(&c->rep_sizes, sizeof(int64_t) * nparts));
     KM_HIP(hipMalloc(&c->rep_bases, sizeof(int64_t) * nparts));
     KM_HIP(hipMemcpy(c->rep_sizes, sizes, sizeof(int64_t) * nparts, hipMemcpyHostToDevice));
@@ -819,8 +840,11 @@ int km_batch_begin(km_ctx* c) {
   return KM_OK;
 }
 
+static int finish_update(km_ctx* c, int slot, bool fold_prep);
+
 int km_update_async(km_ctx* c, double tol, int64_t empty_seed) {
   KM_REQUIRE(c && c->have_c && c->in_batch, KM_ERR_STATE, "km_update_async: call km_batch_begin first");
+  KM_REQUIRE(!c->rep_wait, KM_ERR_STATE, "km_update_async: the last iteration's km_repair_apply_async is missing");
   KM_REQUIRE(c->batch_n < KM_MAX_BATCH, KM_ERR_ARG, "km_update_async: more than KM_MAX_BATCH iterations in a batch");
   KM_REQUIRE(tol >= 0.0, KM_ERR_ARG, "km_update_async: tolerance must be >= 0");
   KM_HIP(hipSetDevice(c->device));
@@ -842,11 +866,30 @@ int km_update_async(km_ctx* c, double tol, int64_t empty_seed) {
     KM_REQUIRE(empty_seed >= 0, KM_ERR_ARG, "km_update_async: negative empty-cluster seed");
     const int rc = ensure_repair(c);
     if (rc != KM_OK) return rc;
+    if (c->rep_mode == 2) {
+      // rows spread over ranks: the caller all-reduces km_repair_buffer, then
+      // km_repair_apply_async finishes this iteration
+      KM_HIP(km::launch_repair_pick(c->gate, c->hist_counts + (size_t)slot * c->g.k, c->g, c->rep_total,
+                                    -std::log(0.00005), (uint64_t)empty_seed, c->rep_empty, c->rep_pcounts,
+                                    c->rep_picks, c->rep_samples, c->rep_cp, c->rep_sizes, c->rep_bases,
+                                    c->rep_nparts, c->X, c->rep_row0, c->hist + slot, c->rep_rows, c->rep_pending,
+                                    c->stream));
+      c->rep_wait = true;
+      c->rep_tol = tol;
+      c->rep_fold = fold_prep;
+      return KM_OK;
+    }
     KM_HIP(km::launch_repair(c->gate, c->hist_counts + (size_t)slot * c->g.k, c->g, c->rep_total,
                              -std::log(0.00005), (uint64_t)empty_seed, c->rep_empty, c->rep_pcounts, c->rep_picks,
                              c->rep_samples, c->rep_cp, c->rep_sizes, c->rep_bases, c->rep_nparts, c->X,
                              c->rep_row0, c->C64_cur, c->C64_new, c->hist + slot, tol, c->stream));
   }
+  return finish_update(c, slot, fold_prep);
+}
+
+// the tail of an iteration enqueued in a batch: slot bookkeeping and the
+// speculative commit of the new centroids
+static int finish_update(km_ctx* c, int slot, bool fold_prep) {
   c->slot_cur[slot] = c->C64_cur;
   c->slot_new[slot] = c->C64_new;
   // speculative commit (kmeans_spark.py:307): the next iteration reads the
@@ -863,6 +906,45 @@ int km_update_async(km_ctx* c, double tol, int64_t empty_seed) {
   return KM_OK;
 }
 
+int km_repair_state(km_ctx* c, int32_t* armed, int32_t* waiting) {
+  KM_REQUIRE(c && armed && waiting, KM_ERR_ARG, "km_repair_state: null argument");
+  *armed = (c->rep_enabled && c->rep_armed) ? 1 : 0;
+  *waiting = c->rep_wait ? 1 : 0;
+  return KM_OK;
+}
+
+int km_repair_buffer(km_ctx* c, void** p, int64_t* len) {
+  KM_REQUIRE(c && p && len, KM_ERR_ARG, "km_repair_buffer: null argument");
+  KM_REQUIRE(c->rep_mode == 2 && c->have_c, KM_ERR_STATE, "km_repair_buffer: needs km_set_layout mode 2 and centroids");
+  if (!c->rep_rows) {
+    const int rc = ensure_repair(c);
+    if (rc != KM_OK) return rc;
+  }
+  *p = c->rep_rows;
+  *len = (int64_t)c->g.k * c->g.d;
+  return KM_OK;
+}
+
+int km_bind_repair_buffer(km_ctx* c, void* p) {
+  KM_REQUIRE(c && c->rep_mode == 2 && c->have_c, KM_ERR_STATE,
+             "km_bind_repair_buffer: needs km_set_layout mode 2 and centroids");
+  const int rc = ensure_repair(c);
+  if (rc != KM_OK) return rc;
+  c->rep_rows = p ? reinterpret_cast<double*>(p) : c->rep_rows_own;
+  return KM_OK;
+}
+
+int km_repair_apply_async(km_ctx* c) {
+  KM_REQUIRE(c && c->in_batch && c->rep_wait, KM_ERR_STATE,
+             "km_repair_apply_async: no repair pick pending (km_update_async in layout mode 2)");
+  KM_HIP(hipSetDevice(c->device));
+  const int slot = c->batch_n;
+  KM_HIP(km::launch_repair_apply(c->gate, c->g, c->rep_empty, c->C64_cur, c->C64_new, c->hist + slot, c->rep_tol,
+                                 c->rep_rows, c->rep_pending, c->stream));
+  c->rep_wait = false;
+  return finish_update(c, slot, c->rep_fold);
+}
+
 int km_batch_end(km_ctx* c, km_status* st, int64_t* counts, int32_t* n_ran) {
   KM_REQUIRE(c && c->in_batch, KM_ERR_STATE, "km_batch_end: no open batch");
   KM_REQUIRE(n_ran, KM_ERR_ARG, "km_batch_end: null n_ran");
@@ -877,6 +959,7 @@ int km_batch_end(km_ctx* c, km_status* st, int64_t* counts, int32_t* n_ran) {
   KM_HIP(hipStreamSynchronize(c->stream));
   c->in_batch = false;
   c->batch_n = 0;
+  c->rep_wait = false;  // an iteration left without its km_repair_apply_async did not run
   int ran = 0;
   while (ran < m && c->hist_host[ran].ran) ++ran;
   *n_ran = ran;

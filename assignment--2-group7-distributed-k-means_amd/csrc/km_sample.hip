@@ -283,27 +283,25 @@ __global__ __launch_bounds__(64) void k_rep_bernoulli(const int* __restrict__ ga
 // (PySpark would retry with rand.randint(0, sys.maxsize); p < 5e-5 by the
 // choice of fraction) or an overflowing partition stops the batch
 // (KM_STOP_EMPTY) and the host repairs.
-__global__ __launch_bounds__(256) void k_rep_finish(const int* __restrict__ gate_ro, int* __restrict__ gate,
-                                                    DevStatus* __restrict__ st, const int64_t* __restrict__ counts,
-                                                    int k, int64_t total, uint64_t seed, int nparts, int cp,
-                                                    int32_t* __restrict__ pcounts, const int64_t* __restrict__ picks,
-                                                    int64_t* __restrict__ samples, int32_t* __restrict__ empty,
-                                                    const float* __restrict__ X, int64_t row0, int64_t n_local,
-                                                    int d, int dp, const double* __restrict__ C_old,
-                                                    double* __restrict__ C_new, double tol) {
+//
+// rep_select: the common first part (returns false when the repair is not
+// this launch's to do: gate raised, no empties, or a stop for the host).
+// It leaves empty[0..num) and samples[0..num) (global rows) in place.
+__device__ bool rep_select(const int* __restrict__ gate_ro, int* __restrict__ gate, DevStatus* __restrict__ st,
+                           const int64_t* __restrict__ counts, int k, int64_t total, uint64_t seed, int nparts,
+                           int cp, int32_t* __restrict__ pcounts, const int64_t* __restrict__ picks,
+                           int64_t* __restrict__ samples, int32_t* __restrict__ empty, uint32_t* mt) {
   __shared__ int wsum[4];
-  __shared__ int s_total, s_ok, s_nf;
-  __shared__ unsigned long long s_max;
-  __shared__ uint32_t mt[624];
+  __shared__ int s_total, s_ok;
   const int num = st->n_empty;
-  if (*gate_ro || num == 0) return;
+  if (*gate_ro || num == 0) return false;
   const int t = threadIdx.x, nt = blockDim.x;
   if ((int64_t)num >= total) {  // takeSample's "every row" branch: left to the host
     if (t == 0) {
       st->stop = KM_STOP_EMPTY;
       *gate = KM_STOP_EMPTY;
     }
-    return;
+    return false;
   }
   // ascending list of the empty clusters (chunk per thread, block prefix)
   {
@@ -333,8 +331,6 @@ __global__ __launch_bounds__(256) void k_rep_finish(const int* __restrict__ gate
     }
     s_total = tot;
     s_ok = (!ovf && tot >= num) ? 1 : 0;
-    s_nf = 0;
-    s_max = 0ull;
   }
   __syncthreads();
   if (!s_ok) {
@@ -342,7 +338,9 @@ __global__ __launch_bounds__(256) void k_rep_finish(const int* __restrict__ gate
       st->stop = KM_STOP_EMPTY;
       *gate = KM_STOP_EMPTY;
     }
-    return;
+    __syncthreads();
+    for (int p = t; p < nparts; p += nt) pcounts[p] = 0;
+    return false;
   }
   if (t == 0) {
     // the picks in partition order (rows ascending within a partition), then
@@ -360,15 +358,34 @@ __global__ __launch_bounds__(256) void k_rep_finish(const int* __restrict__ gate
     }
   }
   __syncthreads();
-  // samples[:num] replace the empty clusters in ascending order (L196-200)
+  // the partition counters start at zero for the next repair
+  for (int p = t; p < nparts; p += nt) pcounts[p] = 0;
+  return true;
+}
+
+// rows rows[i] (i < num, from a device buffer or from X) replace the empty
+// clusters empty[i] (L196-200); their shifts enter max_shift; then the
+// convergence / NaN decision of the iteration
+__device__ void rep_apply(int* __restrict__ gate, DevStatus* __restrict__ st, const int32_t* __restrict__ empty,
+                          int num, int d, const double* __restrict__ C_old, double* __restrict__ C_new, double tol,
+                          const int64_t* __restrict__ samples, const float* __restrict__ X, int64_t row0,
+                          int64_t n_local, int dp, const double* __restrict__ rows) {
+  __shared__ int s_nf;
+  __shared__ unsigned long long s_max;
+  const int t = threadIdx.x, nt = blockDim.x;
+  if (t == 0) {
+    s_nf = 0;
+    s_max = 0ull;
+  }
+  __syncthreads();
   for (int i = t; i < num; i += nt) {
     const int j = empty[i];
-    const int64_t r = samples[i] - row0;
     double sh = 0.0;
     int nf = 0;
-    if (r >= 0 && r < n_local) {
+    const int64_t r = rows ? 0 : samples[i] - row0;
+    if (rows || (r >= 0 && r < n_local)) {
       for (int f = 0; f < d; ++f) {
-        const double v = (double)X[(size_t)r * dp + f];
+        const double v = rows ? rows[(size_t)i * d + f] : (double)X[(size_t)r * dp + f];
         const double df = v - C_old[(size_t)j * d + f];
         C_new[(size_t)j * d + f] = v;
         sh = fma(df, df, sh);
@@ -394,8 +411,54 @@ __global__ __launch_bounds__(256) void k_rep_finish(const int* __restrict__ gate
     st->repaired = 1;
     if (stop) *gate = stop;
   }
-  // the partition counters start at zero for the next repair
-  for (int p = t; p < nparts; p += nt) pcounts[p] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_rep_finish(const int* __restrict__ gate_ro, int* __restrict__ gate,
+                                                    DevStatus* __restrict__ st, const int64_t* __restrict__ counts,
+                                                    int k, int64_t total, uint64_t seed, int nparts, int cp,
+                                                    int32_t* __restrict__ pcounts, const int64_t* __restrict__ picks,
+                                                    int64_t* __restrict__ samples, int32_t* __restrict__ empty,
+                                                    const float* __restrict__ X, int64_t row0, int64_t n_local,
+                                                    int d, int dp, const double* __restrict__ C_old,
+                                                    double* __restrict__ C_new, double tol) {
+  __shared__ uint32_t mt[624];
+  if (!rep_select(gate_ro, gate, st, counts, k, total, seed, nparts, cp, pcounts, picks, samples, empty, mt)) return;
+  rep_apply(gate, st, empty, st->n_empty, d, C_old, C_new, tol, samples, X, row0, n_local, dp, nullptr);
+}
+
+// Rows spread over ranks (km_set_layout mode 2): every rank runs the same
+// Bernoulli passes over ALL partitions (index-level, seeded identically), so
+// every rank picks the same rows; k_rep_pick writes the picked rows it holds
+// into rows[i] and zeros for the others, the caller sum-all-reduces rows over
+// the ranks (stream-ordered), and k_rep_apply puts them in place.  Exact: a
+// row plus zeros is the row.
+__global__ __launch_bounds__(256) void k_rep_pick(const int* __restrict__ gate_ro, int* __restrict__ gate,
+                                                  DevStatus* __restrict__ st, const int64_t* __restrict__ counts,
+                                                  int k, int64_t total, uint64_t seed, int nparts, int cp,
+                                                  int32_t* __restrict__ pcounts, const int64_t* __restrict__ picks,
+                                                  int64_t* __restrict__ samples, int32_t* __restrict__ empty,
+                                                  const float* __restrict__ X, int64_t row0, int64_t n_local, int d,
+                                                  int dp, double* __restrict__ rows, int32_t* __restrict__ pending) {
+  __shared__ uint32_t mt[624];
+  const bool go = rep_select(gate_ro, gate, st, counts, k, total, seed, nparts, cp, pcounts, picks, samples, empty, mt);
+  if (threadIdx.x == 0) *pending = go ? st->n_empty : 0;
+  if (!go) return;
+  const int num = st->n_empty;
+  for (int e = threadIdx.x; e < num * d; e += blockDim.x) {
+    const int i = e / d, f = e - i * d;
+    const int64_t r = samples[i] - row0;
+    rows[e] = (r >= 0 && r < n_local) ? (double)X[(size_t)r * dp + f] : 0.0;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rep_apply(int* __restrict__ gate, DevStatus* __restrict__ st,
+                                                   const int32_t* __restrict__ empty, int d,
+                                                   const double* __restrict__ C_old, double* __restrict__ C_new,
+                                                   double tol, const double* __restrict__ rows,
+                                                   const int32_t* __restrict__ pending) {
+  const int num = *pending;  // 0: no repair this iteration (or a stop already raised)
+  if (num == 0 || *gate) return;
+  rep_apply(gate, st, empty, num, d, C_old, C_new, tol, nullptr, nullptr, 0, 0, 0, rows);
 }
 
 }  // namespace
@@ -408,6 +471,25 @@ hipError_t launch_repair(int* gate, const int64_t* counts, const Geometry& g, in
                      bases, picks, cp, pcounts);
   hipLaunchKernelGGL(k_rep_finish, dim3(1), dim3(256), 0, s, gate, gate, st, counts, g.k, total, seed, nparts, cp,
                      pcounts, picks, samples, empty, X, row0, g.n, g.d, g.dp, C_old, C_new, tol);
+  return hipGetLastError();
+}
+
+hipError_t launch_repair_pick(int* gate, const int64_t* counts, const Geometry& g, int64_t total,
+                              double neg_log_delta, uint64_t seed, int32_t* empty, int32_t* pcounts, int64_t* picks,
+                              int64_t* samples, int cp, const int64_t* sizes, const int64_t* bases, int nparts,
+                              const float* X, int64_t row0, DevStatus* st, double* rows, int32_t* pending,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(k_rep_bernoulli, dim3(nparts), dim3(64), 0, s, gate, st, total, neg_log_delta, seed, sizes,
+                     bases, picks, cp, pcounts);
+  hipLaunchKernelGGL(k_rep_pick, dim3(1), dim3(256), 0, s, gate, gate, st, counts, g.k, total, seed, nparts, cp,
+                     pcounts, picks, samples, empty, X, row0, g.n, g.d, g.dp, rows, pending);
+  return hipGetLastError();
+}
+
+hipError_t launch_repair_apply(int* gate, const Geometry& g, const int32_t* empty, const double* C_old,
+                               double* C_new, DevStatus* st, double tol, const double* rows, const int32_t* pending,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(k_rep_apply, dim3(1), dim3(256), 0, s, gate, st, empty, g.d, C_old, C_new, tol, rows, pending);
   return hipGetLastError();
 }
 

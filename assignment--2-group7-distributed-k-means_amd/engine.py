@@ -132,7 +132,7 @@ class HipEngine:
     def assign_stats(self) -> None:
         self._c(self.lib.km_assign_stats(self.ctx), "km_assign_stats")
 
-    def run_collective(self, fn) -> None:
+    def run_collective(self, fn, tensor=None) -> None:
         """Run ``fn(stats_tensor, async_op=True)`` (an in-place all-reduce)
         ordered on this context's HIP stream, with no host synchronisation.
 
@@ -147,7 +147,7 @@ class HipEngine:
         km_update_async enqueued next on the engine stream read the summed
         buffer.  gloo (CPU tensors) completes inside wait()."""
         with self._torch.cuda.stream(self._tstream):
-            work = fn(self._stats_t, async_op=True)
+            work = fn(self._stats_t if tensor is None else tensor, async_op=True)
             if work is not None:
                 work.wait()
 
@@ -164,12 +164,40 @@ class HipEngine:
     def update_async(self, tol: float, empty_seed: int = 0) -> None:
         self._c(self.lib.km_update_async(self.ctx, float(tol), int(empty_seed)), "km_update_async")
 
-    def set_layout(self, sizes, row0: int, device_repair: bool) -> None:
+    def set_layout(self, sizes, row0: int, device_repair: int) -> None:
         """The dataset's takeSample partition layout; device_repair moves the
-        empty-cluster repair onto the GPU (one rank holding every row)."""
+        empty-cluster repair onto the GPU: 1 = one rank holding every row,
+        2 = rows spread over ranks (the caller all-reduces the repair rows,
+        ``repair_exchange``)."""
         sizes = np.ascontiguousarray(sizes, dtype=np.int64)
-        self._c(self.lib.km_set_layout(self.ctx, _ptr(sizes, _PI64), len(sizes), int(row0), 1 if device_repair else 0),
+        self._c(self.lib.km_set_layout(self.ctx, _ptr(sizes, _PI64), len(sizes), int(row0), int(device_repair)),
                 "km_set_layout")
+        self._rep_mode = int(device_repair)
+        self._rep_t = None
+
+    def repair_state(self) -> Tuple[bool, bool]:
+        """(armed, waiting): the next km_update_async may enqueue a device
+        repair / the last one left its iteration to repair_apply_async."""
+        a, w = ctypes.c_int32(), ctypes.c_int32()
+        self._c(self.lib.km_repair_state(self.ctx, ctypes.byref(a), ctypes.byref(w)), "km_repair_state")
+        return bool(a.value), bool(w.value)
+
+    def repair_bind(self) -> None:
+        """Layout mode 2: a torch tensor as the repair-row buffer (the one the
+        process group all-reduces); call before enqueueing the iterations."""
+        if self._rep_t is None or self._rep_t.numel() != self.k * self.d:
+            torch = self._torch
+            self._rep_t = torch.zeros(self.k * self.d, dtype=torch.float64, device=f"cuda:{self.device}")
+            torch.cuda.synchronize(self.device)
+            self._c(self.lib.km_bind_repair_buffer(self.ctx, ctypes.c_void_p(self._rep_t.data_ptr())),
+                    "km_bind_repair_buffer")
+
+    def repair_exchange(self, allreduce) -> None:
+        """Layout mode 2: sum the ranks' picked replacement rows (each holds
+        its own, zeros elsewhere) on this context's stream, then finish the
+        iteration on the device (km_repair_apply_async)."""
+        self.run_collective(allreduce, self._rep_t)
+        self._c(self.lib.km_repair_apply_async(self.ctx), "km_repair_apply_async")
 
     def batch_end(self, m: int):
         """Sync once; [(status, counts)] of the iterations of the batch that ran

@@ -54,11 +54,19 @@ class LloydRunner:
             self.engine.load_blobs(pl.n_local, b.d, pl.row0, b.n_centers, b.box, b.std, b.seed)
         else:
             self.engine.load_host(pl.local_rows)
-        # one rank holding every row: empty clusters are repaired on the device
-        # (takeSample policy, kmeans_spark.py:191-204) without stopping a batch
-        self.device_repair = self.comm.world == 1 and hasattr(self.engine, "set_layout")
+        # empty clusters are repaired on the device (takeSample policy,
+        # kmeans_spark.py:191-204) without stopping a batch: mode 1 with one
+        # rank holding every row; mode 2 with the rows spread over ranks (every
+        # rank picks the same rows, the owners contribute them to one
+        # stream-ordered all-reduce, LloydRunner.run)
+        self.device_repair = 0
+        if hasattr(self.engine, "set_layout"):
+            if self.comm.world == 1:
+                self.device_repair = 1
+            elif hasattr(self.engine, "repair_exchange") and getattr(self.engine, "distributed", False):
+                self.device_repair = 2
         if self.device_repair:
-            self.engine.set_layout(pl.global_sizes, 0, True)
+            self.engine.set_layout(pl.global_sizes, pl.row0 if self.device_repair == 2 else 0, self.device_repair)
 
     def rows(self, gidx: List[int]) -> np.ndarray:
         """Rows by global index (what ``rdd.takeSample`` returns, L72/L196):
@@ -88,13 +96,22 @@ class LloydRunner:
         size = self.batch
         while it < max_iter:
             m = min(size, max_iter - it)
+            seed = model._empty_seed()                         # int(time.time()), L196
+            if self.device_repair == 2:
+                eng.repair_bind()
+                if eng.repair_state()[0]:                      # armed: every rank needs the same seed
+                    seed = self.comm.broadcast_obj(seed)
             eng.batch_begin()
             try:
                 for _ in range(m):
                     eng.assign_stats()                         # L272 (+ L169-171 map side)
                     self.comm.allreduce_stats(eng)             # L169-173 shuffle + collect
-                    # L176-206 (+ the repair's seed int(time.time()), L196), device convergence test
-                    eng.update_async(model.tolerance, model._empty_seed())
+                    # L176-206 (+ the repair's seed, L196), device convergence test
+                    eng.update_async(model.tolerance, seed)
+                    if self.device_repair == 2 and eng.repair_state()[1]:
+                        # the picked rows from their owners (L196-200), then the rest
+                        # of the update on the device
+                        eng.repair_exchange(self.comm.dist.all_reduce)
             except BaseException:
                 # close the batch (the gate comes down, the context is back to
                 # the last iteration that ran), then report the original error

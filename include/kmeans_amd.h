@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KM_ABI_VERSION 3
+#define KM_ABI_VERSION 4
 
 #define KM_OK 0
 #define KM_EMPTY 1          /* informational: the update found empty clusters */
@@ -153,6 +153,23 @@ int km_update(km_ctx* ctx, km_status* st, int64_t* counts);
  * retry PySpark's resampling loop) empty clusters stop the batch and the
  * caller repairs them on the host with the same policy. */
 int km_set_layout(km_ctx* ctx, const int64_t* sizes, int32_t nparts, int64_t row0, int32_t device_repair);
+/* device_repair = 2 (ABI 4): the rows are spread over ranks, this context
+ * holding global rows [row0, row0 + n).  Every rank runs the same takeSample
+ * passes over all partitions (index level), so all pick the same rows; then,
+ * for an iteration whose km_update_async left the repair waiting
+ * (km_repair_state: waiting = 1), the caller sum-all-reduces the repair
+ * buffer (km_repair_buffer: k*d doubles, each rank contributing the picked
+ * rows it holds and zeros) on the context's stream, and km_repair_apply_async
+ * puts the rows in place and finishes the iteration -- no host round trip.
+ * Replaces the driver-side takeSample + broadcast of kmeans_spark.py:191-204
+ * when the rows sit on several GPUs.  The seed passed to km_update_async must
+ * be the same on every rank. */
+int km_repair_state(km_ctx* ctx, int32_t* armed, int32_t* waiting);
+int km_repair_buffer(km_ctx* ctx, void** buffer, int64_t* len);
+/* use an external device buffer of k*d doubles (e.g. a torch tensor that the
+ * process group all-reduces); NULL restores the context's own */
+int km_bind_repair_buffer(km_ctx* ctx, void* buffer);
+int km_repair_apply_async(km_ctx* ctx);
 /* Batches of Lloyd iterations without host synchronisation (replaces the
  * per-iteration driver round trip of kmeans_spark.py:266-313).  Between
  * km_batch_begin and km_batch_end the caller enqueues up to KM_MAX_BATCH

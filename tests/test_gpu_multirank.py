@@ -59,16 +59,22 @@ def _rank_main(rank, world, port, name, q):
             km.fit(rdd, sc)
         labels = np.array(km.predict(rdd, sc).collect())
         assert km._runner.engine.distributed
-        q.put((rank, km.centroids, km.sse_history, labels, buf.getvalue(), km._runner.pl.n_local))
+        assert km._runner.device_repair == 2
+        q.put((rank, km.centroids, km.sse_history, labels, buf.getvalue(), km._runner.pl.n_local,
+               km._runner.device_repairs))
     except Exception as e:  # surface the failure in the parent
-        q.put((rank, repr(e), None, None, None, None))
+        q.put((rank, repr(e), None, None, None, None, None))
         raise
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["test_a", "empty", "c3_small"])
+@pytest.mark.parametrize("name", ["test_a", "empty", "c3_small", "c5_poor"])
 def test_two_ranks_on_gpu_match_reference(golden, name):
+    # "empty" and "c5_poor" (k = 512, ~509 empty clusters at the first update)
+    # repair their empty clusters on the devices of both ranks (layout mode 2:
+    # same picks on every rank, rows from their owners through one
+    # stream-ordered all-reduce), with no host round trip
     import torch.multiprocessing as mp
     g = golden(name)
     ctx = mp.get_context("spawn")
@@ -82,8 +88,10 @@ def test_two_ranks_on_gpu_match_reference(golden, name):
         p.join(60)
         assert p.exitcode == 0, res
     assert sum(r[5] for r in res) == len(g["X"])  # the shards partition the rows
-    for rank, C, sse, labels, out, _ in res:
+    for rank, C, sse, labels, out, _, reps in res:
         np.testing.assert_allclose(C, g["centroids"], rtol=1e-9, atol=1e-9)
         np.testing.assert_allclose(sse, g["sse_history"], rtol=1e-9)
         np.testing.assert_array_equal(labels, g["labels"])
+        if name in ("empty", "c5_poor"):
+            assert reps > 0, "the empty clusters were not repaired on the device"
     assert res[0][4] and not res[1][4]  # only rank 0 logs
