@@ -103,3 +103,79 @@ def test_rccl_allreduce_ordered_on_engine_stream():
     C6_batch, sse_batch = out["batch"]
     np.testing.assert_allclose(sse_batch, sse6, rtol=1e-9)
     np.testing.assert_allclose(C6_batch, C6, rtol=1e-9, atol=1e-9)
+
+
+def _child_repair(port, q):
+    # layout mode 2 (rows spread over ranks) driven through RCCL at world 1:
+    # the repair rows go through the same stream-ordered all-reduce as on 8
+    # GPUs; the c5_poor golden (k = 512, ~509 empty clusters at the first
+    # update, reference-generated) must come out exactly
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        import kmeans_amd as ka
+        from kmeans_amd.engine import HipEngine
+        from conftest import load_golden
+        g = load_golden("c5_poor")
+        X = g["X"]
+        rdd = ka.LocalContext().parallelize(X, int(g["slices"]))
+        sizes = [rdd.partition_len(i) for i in range(rdd.getNumPartitions())]
+        k, tol, seed = int(g["k"]), float(g["tol"]), int(g["time_seed"])
+        eng = HipEngine(0, distributed=True)
+        eng.load_host(X)
+        eng.set_layout(sizes, 0, 2)
+        eng.set_sse(bool(g["sse"]))
+        eng.set_centroids(g["init"])
+        sse, it, repaired, waited = [], 0, 0, 0
+        max_iter = int(g["max_iter"])
+        while it < max_iter:
+            m = min(4, max_iter - it)
+            eng.repair_bind()
+            eng.batch_begin()
+            for _ in range(m):
+                eng.assign_stats()
+                eng.run_collective(dist.all_reduce)
+                eng.update_async(tol, seed)
+                if eng.repair_state()[1]:
+                    waited += 1
+                    eng.repair_exchange(dist.all_reduce)
+            recs = eng.batch_end(m)
+            for st, _ in recs:
+                sse.append(st.sse)
+                repaired += int(st.repaired)
+            it += len(recs)
+            last = recs[-1][0]
+            assert last.stop_reason != 2, "empty stop: the device repair did not run"
+            eng.commit()
+            if last.stop_reason == 1:
+                break
+        q.put({"C": eng.get_centroids(0), "sse": sse, "repaired": repaired, "waited": waited,
+               "ref": (g["centroids"], g["sse_history"])})
+        eng.close()
+    except Exception as e:  # report, do not hang the parent
+        q.put({"error": repr(e)})
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_device_repair_with_rows_over_ranks():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_child_repair, args=(_port(), q))
+    p.start()
+    out = q.get(timeout=240)
+    p.join(60)
+    assert "error" not in out, out.get("error")
+    assert p.exitcode == 0
+    assert out["repaired"] > 0 and out["waited"] > 0
+    C, sse = out["ref"]
+    np.testing.assert_allclose(out["sse"], sse, rtol=1e-9)
+    np.testing.assert_allclose(out["C"], C, rtol=1e-9, atol=1e-9)

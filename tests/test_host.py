@@ -603,3 +603,90 @@ def test_graft_build_entry_matches_the_library_abi():
     # against the package constant; a stale pin here once broke it
     import __graft_entry__ as g
     g.build()
+
+
+# ------------------------------------------- distributed device repair (order)
+def test_distributed_device_repair_enqueue_order():
+    # layout mode 2 (rows spread over ranks): per iteration the runner must
+    # enqueue assign -> stats all-reduce -> update (with ONE seed shared by the
+    # ranks, broadcast only while the repair is armed) -> the repair rows'
+    # all-reduce -> km_repair_apply_async, all without a host sync; a batch
+    # that is not armed enqueues no repair collective (kmeans_spark.py:191-204)
+    from kmeans_amd import _lib
+    from kmeans_amd.dataset import Placement
+    from kmeans_amd.kmeans import LloydRunner
+    calls = []
+
+    class Dist:
+        @staticmethod
+        def all_reduce(t, async_op=False):
+            calls.append("allreduce_rows")
+
+    class Comm:
+        rank, world, dist = 0, 2, Dist
+
+        def broadcast_obj(self, obj, src=0):
+            calls.append(("bcast", obj))
+            return 777
+
+        def allreduce_stats(self, eng):
+            calls.append("allreduce_stats")
+
+    class Eng:
+        distributed = True
+        armed, waiting = True, False
+
+        def load_host(self, rows):
+            pass
+
+        def set_layout(self, sizes, row0, mode):
+            calls.append(("layout", list(sizes), row0, mode))
+
+        def repair_bind(self):
+            calls.append("bind")
+
+        def repair_state(self):
+            return self.armed, self.waiting
+
+        def batch_begin(self):
+            calls.append("begin")
+
+        def assign_stats(self):
+            calls.append("assign")
+
+        def update_async(self, tol, seed):
+            calls.append(("update", seed))
+            self.waiting = self.armed
+
+        def repair_exchange(self, fn):
+            fn(None, async_op=True)
+            calls.append("apply")
+            self.waiting = False
+
+        def batch_end(self, m):
+            st = _lib.KmStatus()
+            st.ran = 1
+            st.max_shift = 1.0
+            self.armed = False          # a batch without empties disarms
+            return [(st, np.ones(2, dtype=np.int64))] * m
+
+        def commit(self):
+            calls.append("commit")
+
+    class Model:
+        tolerance, compute_sse = 1e-300, False
+
+        @staticmethod
+        def _empty_seed():
+            return 123
+
+    pl = Placement(global_sizes=[6, 6], local_rows=np.zeros((6, 3)), row0=6, n_local=6, n_global=12, d=3,
+                   dtype=np.float64)
+    run = LloydRunner(Eng(), pl, Comm(), 2)
+    run.load()
+    assert run.device_repair == 2 and calls[0] == ("layout", [6, 6], 6, 2)
+    run.batch = 2
+    run.run(Model(), None, 4)
+    it = ["assign", "allreduce_stats", ("update", 777), "allreduce_rows", "apply"]
+    assert calls[1:] == ["bind", ("bcast", 123), "begin"] + it + it + ["commit", "bind", "begin"] + \
+        ["assign", "allreduce_stats", ("update", 123)] * 2 + ["commit"], calls
