@@ -75,6 +75,69 @@ __device__ inline double np_pw(const SQ& sq, int lo, int n) {
   }
 }
 
+// Two norms in lockstep (one lane): SQ2(f, ta, tb) yields the terms of both
+// at feature f, so a centroid value read once serves two points; each sum
+// keeps NumPy's pairwise order exactly as np_pw_block / np_pw do.
+template <class SQ2>
+__device__ inline void np_pw2_block(const SQ2& sq, int lo, int n, double& sa, double& sb) {
+#pragma clang fp contract(off)
+  if (n < 8) {
+    double ra = 0.0, rb = 0.0;
+    for (int i = 0; i < n; ++i) {
+      double ta, tb;
+      sq(lo + i, ta, tb);
+      ra = np_add(ra, ta);
+      rb = np_add(rb, tb);
+    }
+    sa = ra;
+    sb = rb;
+    return;
+  }
+  double ra[8], rb[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) sq(lo + u, ra[u], rb[u]);
+  const int nm = n - (n & 7);
+  int i = 8;
+  for (; i < nm; i += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      double ta, tb;
+      sq(lo + i + u, ta, tb);
+      ra[u] = np_add(ra[u], ta);
+      rb[u] = np_add(rb[u], tb);
+    }
+  }
+  double xa = np_combine8(ra), xb = np_combine8(rb);
+  for (; i < n; ++i) {
+    double ta, tb;
+    sq(lo + i, ta, tb);
+    xa = np_add(xa, ta);
+    xb = np_add(xb, tb);
+  }
+  sa = xa;
+  sb = xb;
+}
+
+template <int DEPTH, class SQ2>
+__device__ inline void np_pw2(const SQ2& sq, int lo, int n, double& sa, double& sb) {
+#pragma clang fp contract(off)
+  if constexpr (DEPTH == 0) {
+    np_pw2_block(sq, lo, n, sa, sb);
+  } else {
+    if (n <= 128) {
+      np_pw2_block(sq, lo, n, sa, sb);
+      return;
+    }
+    int n2 = n >> 1;
+    n2 -= n2 & 7;
+    double a1, b1, a2, b2;
+    np_pw2<DEPTH - 1>(sq, lo, n2, a1, b1);
+    np_pw2<DEPTH - 1>(sq, lo + n2, n - n2, a2, b2);
+    sa = np_add(a1, a2);
+    sb = np_add(b1, b2);
+  }
+}
+
 // np.linalg.norm of one centroid row: two halvings suffice for d <= 256 (a
 // half of n <= 256 has at most n/2 + 8 terms), five for d <= 2048 (wide rows)
 template <int DEPTH, class SQ>

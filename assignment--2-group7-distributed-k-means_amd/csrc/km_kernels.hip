@@ -3348,15 +3348,36 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
       __syncthreads();
       if (lane < cw) {
         const double* ct = sCT + lane;
+        // the wave's entries in pairs: each chunk value read once for two
+        // points (np_pw2, NumPy's order for each); a pair with one entry
+        // already resolved (chain scan) or past the end still evaluates the
+        // other -- the decision is per entry, never per pair.  The running
+        // minima are updated with selects, not branches: the branchy form
+        //   if (have[g + 1] && np_better(vb, ...)) { best[g + 1] = vb; ... }
+        // loses every update after the first chunk on this toolchain (the
+        // per-chunk norms are right, the lane minima stay at chunk 0:
+        // DESIGN.md section 2, "The lockstep full-scan variant"), which is
+        // what made the round-2 lockstep variant return wrong labels.
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-          if (!have[g]) continue;
-          const float* xg = xs + g * d;
-          const double v = np_norm_d<2>([&](int f) { return np_sq(ct[(size_t)f * ch], xg[f]); }, d);
-          if (np_better(v, best[g], bj[g] >= 0)) {
-            best[g] = v;
-            bj[g] = c0 + lane;
-          }
+        for (int g = 0; g < G; g += 2) {
+          if (!have[g] && !have[g + 1]) continue;
+          const float* xa = xs + g * d;
+          const float* xb = xs + (g + 1) * d;
+          double sa, sb;
+          np_pw2<2>(
+              [&](int f, double& ta, double& tb) {
+                const double c = ct[(size_t)f * ch];
+                ta = np_sq(c, xa[f]);
+                tb = np_sq(c, xb[f]);
+              },
+              0, d, sa, sb);
+          const double va = sqrt(sa), vb = sqrt(sb);
+          const bool ua = have[g] && np_better(va, best[g], bj[g] >= 0);
+          const bool ub = have[g + 1] && np_better(vb, best[g + 1], bj[g + 1] >= 0);
+          best[g] = ua ? va : best[g];
+          bj[g] = ua ? c0 + lane : bj[g];
+          best[g + 1] = ub ? vb : best[g + 1];
+          bj[g + 1] = ub ? c0 + lane : bj[g + 1];
         }
       }
     }
