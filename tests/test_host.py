@@ -690,3 +690,22 @@ def test_distributed_device_repair_enqueue_order():
     it = ["assign", "allreduce_stats", ("update", 777), "allreduce_rows", "apply"]
     assert calls[1:] == ["bind", ("bcast", 123), "begin"] + it + it + ["commit", "bind", "begin"] + \
         ["assign", "allreduce_stats", ("update", 123)] * 2 + ["commit"], calls
+
+
+def test_fullscan_lockstep_updates_minima_with_selects():
+    # The lockstep chunk pass of k_fullscan evaluates two queued points per
+    # staged centroid value.  Written as branches
+    #   if (have[g + 1] && np_better(vb, best[g + 1], ...)) { best[g + 1] = vb; ... }
+    # the lane minima of the second point stay at their first-chunk values on
+    # this toolchain (printf trace: per-chunk norms right, minima never
+    # updated; branch exp/fullscan-lockstep-branchy), the
+    # cause of the round-2 lockstep variant's wrong labels.  The GPU test
+    # test_gpu_parity.py::test_one_step_vs_oracle[50000-64-256-256] catches
+    # it at run time; this lint keeps the select form in the source.
+    src = open(os.path.join(ROOT, "assignment--2-group7-distributed-k-means_amd", "csrc", "km_kernels.hip")).read()
+    body = src[src.index("void k_fullscan("):]
+    body = body[:body.index("hipError_t launch_resolve(")]
+    body = re.sub(r"//[^\n]*", "", body)  # code only
+    assert "np_pw2<2>(" in body
+    assert "best[g + 1] = ub ? vb : best[g + 1];" in body
+    assert re.search(r"if \(have\[g \+ 1\] && np_better", body) is None
