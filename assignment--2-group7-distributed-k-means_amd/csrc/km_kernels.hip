@@ -15,6 +15,11 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+// waves per k_assign_mfma workgroup for 64 < dp < 192 (4, 8 or 12)
+#ifndef KM_WIDE_WAVES
+#define KM_WIDE_WAVES 12
+#endif
+
 namespace km {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -683,7 +688,10 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
       const size_t off = (size_t)blk * BLKB + (size_t)t * 1024;
       Frag f;
       f.hi = *reinterpret_cast<const f16x8*>(laneHi + off);
-      f.lo = *reinterpret_cast<const f16x8*>(laneLo + off);
+      if constexpr (ABL == 3)
+        f.lo = f.hi;  // diagnostic: half the LDS fragment reads
+      else
+        f.lo = *reinterpret_cast<const f16x8*>(laneLo + off);
       return f;
     };
     auto mfma3 = [&](f32x16 acc, const Frag& f, int t) {
@@ -1165,7 +1173,8 @@ static int mfma_waves_env() {
 
 static int mfma_kc(const Geometry& g, int* waves) {
   const size_t per = (size_t)g.dp * 4 + 4;
-  *waves = (g.dp >= 192) ? 4 : (g.dp <= 64 ? mfma_waves_env() : 8);
+  static const int wide_waves = diag_env("KM_MFMA_WAVES_X", KM_WIDE_WAVES);  // experiment knob for 64 < dp < 192
+  *waves = (g.dp >= 192) ? 4 : (g.dp <= 64 ? mfma_waves_env() : (wide_waves == 4 || wide_waves == 12 ? wide_waves : 8));
   if ((size_t)g.kp * per <= MFMA_LDS_LARGE) return g.kp;
   return (int)((MFMA_LDS_LARGE / 2 / per) / 64 * 64);  // two chunk buffers
 }
@@ -1211,6 +1220,20 @@ static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, con
       return;
     }
   }
+#ifdef KM_DIAG
+  if constexpr (NS == 8) {  // KM_ABLATE=11 (no key updates) | 12 (MFMA -> adds) | 13 (no lo reads), c5 shape
+    static const int e = diag_env("KM_ABLATE", 0);
+    if (waves == 12 && e >= 11 && e <= 13) {  // instead of the product kernel
+      if (e == 11)
+        hipLaunchKernelGGL((k_assign_mfma<NS, 12, 1>), dim3(blocks), dim3(768), lds, s, a);
+      else if (e == 12)
+        hipLaunchKernelGGL((k_assign_mfma<NS, 12, 2>), dim3(blocks), dim3(768), lds, s, a);
+      else
+        hipLaunchKernelGGL((k_assign_mfma<NS, 12, 3>), dim3(blocks), dim3(768), lds, s, a);
+      return;
+    }
+  }
+#endif
   if constexpr (NS >= 12) {
     hipLaunchKernelGGL((k_assign_mfma<NS, 4>), dim3(blocks), dim3(256), lds, s, a);
   } else {
