@@ -15,7 +15,11 @@
 #include <stdio.h>
 #include <stdlib.h>
 
-// waves per k_assign_mfma workgroup for 64 < dp < 192 (4, 8 or 12)
+// waves per k_assign_mfma workgroup for dp <= 64 (8, 12 or 16) and for
+// 64 < dp < 192 (4, 8 or 12)
+#ifndef KM_NARROW_WAVES
+#define KM_NARROW_WAVES 16
+#endif
 #ifndef KM_WIDE_WAVES
 #define KM_WIDE_WAVES 12
 #endif
@@ -510,7 +514,7 @@ int cand_rec_words() { return CAND_REC; }
 
 template <int NS, int WAVES>
 constexpr int mfma_min_waves() {
-  return WAVES == 4 ? 1 : (WAVES == 12 ? 3 : (NS <= 4 ? 4 : 2));
+  return WAVES == 4 ? 1 : (WAVES == 16 ? 4 : (WAVES == 12 ? 3 : (NS <= 4 ? 4 : 2)));
 }
 
 struct MfmaArgs {
@@ -1167,7 +1171,8 @@ __global__ __launch_bounds__(256, 1) void k_assign_wide(MfmaArgs A, int dp) {
 }
 
 static int mfma_waves_env() {
-  static const int v = diag_env("KM_MFMA_WAVES", 12) == 8 ? 8 : 12;  // experiment knob: 12 (default) or 8
+  static const int e = diag_env("KM_MFMA_WAVES", KM_NARROW_WAVES);  // experiment knob: 8, 12 or 16
+  static const int v = (e == 8 || e == 16) ? e : 12;
   return v;
 }
 
@@ -1213,6 +1218,8 @@ static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, con
     if (mfma_top2(NS)) {
       if (waves == 4)
         hipLaunchKernelGGL((k_assign_mfma<NS, 4, 0, true>), dim3(blocks), dim3(256), lds, s, a);
+      else if (waves == 16)
+        hipLaunchKernelGGL((k_assign_mfma<NS, 16, 0, true>), dim3(blocks), dim3(1024), lds, s, a);
       else if (waves == 12)
         hipLaunchKernelGGL((k_assign_mfma<NS, 12, 0, true>), dim3(blocks), dim3(768), lds, s, a);
       else
@@ -1239,7 +1246,9 @@ static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, con
   } else {
     if (waves == 4)
       hipLaunchKernelGGL((k_assign_mfma<NS, 4>), dim3(blocks), dim3(256), lds, s, a);
-    else if (waves == 12)
+    else if (waves == 16) {
+      if constexpr (NS <= 4) hipLaunchKernelGGL((k_assign_mfma<NS, 16>), dim3(blocks), dim3(1024), lds, s, a);
+    } else if (waves == 12)
       hipLaunchKernelGGL((k_assign_mfma<NS, 12>), dim3(blocks), dim3(768), lds, s, a);
     else
       hipLaunchKernelGGL((k_assign_mfma<NS, 8>), dim3(blocks), dim3(512), lds, s, a);
@@ -3468,6 +3477,9 @@ static constexpr int STATS_LDS = 156 * 1024;
 // The workgroup also owns a feature range [f0, f0 + fr) (blockIdx.z):
 // splitting the features instead of the clusters keeps X read once when
 // k (d+1) doubles exceed LDS but k (fr+1) fit (c4: 1024 clusters x 16 features).
+// PLAIN (diagnostic build, KM_ABLATE=14): LDS read-add-write instead of the
+// float64 LDS atomics (races: results wrong by design), to price the atomics
+template <bool PLAIN = false>
 __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int64_t n, int d, int dp, int k,
                                                 const int32_t* __restrict__ labels, double* __restrict__ stats,
                                                 int kr, int fr, int64_t rows_per_block, const double* __restrict__ C64P,
@@ -3524,10 +3536,17 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
         const int lab = __shfl(labreg, rr & 63);
         if (act && rr < nrow && lab >= c0 && lab < c1) {
           double* t = tab + (lab - c0) * RS + mm;
-          atomicAdd(t, (double)v[u].x);
-          atomicAdd(t + L, (double)v[u].y);
-          atomicAdd(t + 2 * L, (double)v[u].z);
-          atomicAdd(t + 3 * L, (double)v[u].w);
+          if constexpr (PLAIN) {
+            t[0] += (double)v[u].x;
+            t[L] += (double)v[u].y;
+            t[2 * L] += (double)v[u].z;
+            t[3 * L] += (double)v[u].w;
+          } else {
+            atomicAdd(t, (double)v[u].x);
+            atomicAdd(t + L, (double)v[u].y);
+            atomicAdd(t + 2 * L, (double)v[u].z);
+            atomicAdd(t + 3 * L, (double)v[u].w);
+          }
           if (sse) {  // padded features are 0 - 0
             const double* c = C64P + (size_t)lab * dp + f0 + 4 * mm;
             const double2 ca = *reinterpret_cast<const double2*>(c);
@@ -3620,8 +3639,17 @@ hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels
   if (bx > (g.n + min_rows - 1) / min_rows) bx = (g.n + min_rows - 1) / min_rows;
   int64_t rpb = (g.n + bx - 1) / bx;
   rpb = (rpb + 63) / 64 * 64;
-  hipLaunchKernelGGL(k_stats, dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024), lds, s, X, g.n,
-                     g.d, g.dp, g.k, labels, stats, kr, fr, rpb, C64P,
+#ifdef KM_DIAG
+  static const int abl = diag_env("KM_ABLATE", 0);
+  if (abl == 14) {
+    hipLaunchKernelGGL(k_stats<true>, dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024), lds, s, X,
+                       g.n, g.d, g.dp, g.k, labels, stats, kr, fr, rpb, C64P,
+                       C64P ? stats + (size_t)g.k * (g.d + 1) : (double*)nullptr, gate);
+    return hipGetLastError();
+  }
+#endif
+  hipLaunchKernelGGL(k_stats<false>, dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024), lds, s, X,
+                     g.n, g.d, g.dp, g.k, labels, stats, kr, fr, rpb, C64P,
                      C64P ? stats + (size_t)g.k * (g.d + 1) : (double*)nullptr, gate);
   return hipGetLastError();
 }
