@@ -967,29 +967,26 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
 
 // ---------------------------------------------------------------------------
 // Screening for rows wider than 256 features (kmeans_spark.py:153 takes any
-// row length), where the x tile no longer fits the registers whole.  The
-// features go in chunks of WIDE_FW = 256 (16 K-steps, the 32 rows' fp16 hi/lo
-// fragments of one chunk in 128 VGPRs), the centroids in chunks of WIDE_KC =
-// 128 (4 MFMA blocks, 64 accumulators).  For each (centroid chunk, feature
-// chunk) the workgroup stages that piece's fragments in LDS (the lane-linear
-// image of k_assign_mfma, 128 KiB) and every wave runs the 3 MFMAs per block
-// and K-step on its own 32 rows; the accumulators carry the scores across
-// feature chunks, so keys, chains, the rigorous bound and the queue are those
-// of k_assign_mfma (top-3 chains).  X is re-read once per centroid chunk
-// (from L2 for k <= 128: once).
+// row length), where the x tile no longer fits the registers whole.  Pieces of
+// WIDE_KC = 256 centroids x WIDE_FW = 64 features (8 MFMA blocks x 4 K-steps,
+// the lane-linear fp16 hi/lo image of k_assign_mfma, 64 KiB + the chunk's
+// ||c||^2) stream through two LDS buffers by LDS-DMA, one piece ahead, with one
+// barrier per piece; 8 waves (2 per SIMD), each on its own 32 rows, run the 3
+// MFMAs per block and K-step into 8 accumulators (128 VGPRs) carried across
+// the feature pieces, the rows' next feature slice loaded one piece ahead.
+// Keys, chains, the rigorous bound and the queue are those of k_assign_mfma
+// (top-3 chains).  X is read once per centroid chunk (once for k <= 256).
 // ---------------------------------------------------------------------------
-static constexpr int WIDE_KC = 128, WIDE_FW = 256;
+static constexpr int WIDE_KC = 256, WIDE_FW = 64, WIDE_WAVES = 8;
 static constexpr int WIDE_MAX_DP = 2048;  // k_fullscan stages 2 x 8 rows in LDS
+static constexpr size_t WIDE_BUF = 2 * (size_t)(WIDE_KC / 32) * (WIDE_FW / 16) * 1024 + WIDE_KC * 4;
 
-__global__ __launch_bounds__(256, 1) void k_assign_wide(MfmaArgs A, int dp) {
+__global__ __launch_bounds__(WIDE_WAVES * 64, 2) void k_assign_wide(MfmaArgs A, int dp) {
   if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
-  constexpr int NSW = WIDE_FW / 16;  // K-steps per feature chunk
+  constexpr int NSW = WIDE_FW / 16;  // K-steps per feature piece
   constexpr int NBW = WIDE_KC / 32;  // MFMA blocks per centroid chunk
-  constexpr int BLKB = NSW * 1024;   // bytes of one block's fragments (one of hi / lo)
+  constexpr int HIMG = NBW * NSW * 1024;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* sHi = smem;
-  char* sLo = smem + NBW * BLKB;
-  float* sCn = reinterpret_cast<float*>(smem + 2 * NBW * BLKB);
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -1005,35 +1002,45 @@ __global__ __launch_bounds__(256, 1) void k_assign_wide(MfmaArgs A, int dp) {
   const float rho = __builtin_ldexpf(1.0f, b - 2 - 23) * 1.01f;  // key truncation (relative)
   const int nkc = (kp + WIDE_KC - 1) / WIDE_KC;
   const int nfc = (dp + WIDE_FW - 1) / WIDE_FW;
+  const int npc = nkc * nfc;  // pieces per tile group
   const int64_t ntiles = (n + 31) / 32;
-  const int64_t nwt = (ntiles + 3) / 4;
+  const int64_t nwt = (ntiles + WIDE_WAVES - 1) / WIDE_WAVES;
 
-  // piece (blk, t) of centroid chunk ch / feature chunk fc at byte (blk NSW + t) KiB
-  auto stage = [&](int ch, int fc, int nb, int ns) {
-    for (int id = threadIdx.x; id < nb * NSW * 64; id += 256) {
-      const int l = id & 63;
-      const int bt = id >> 6;
-      const int blk = bt / NSW, t = bt - blk * NSW;
-      if (t >= ns) continue;
-      const size_t src = (size_t)(ch * WIDE_KC + blk * 32 + (l & 31)) * dp + fc * WIDE_FW + 16 * t + 8 * (l >> 5);
-      *reinterpret_cast<uint4*>(sHi + (size_t)id * 16) = *reinterpret_cast<const uint4*>(A.Chi + src);
-      *reinterpret_cast<uint4*>(sLo + (size_t)id * 16) = *reinterpret_cast<const uint4*>(A.Clo + src);
+  // piece pc = ch * nfc + fc into buffer bf: fragment (blk, t) at (blk NSW + t)
+  // KiB of each image, one 1 KiB LDS-DMA per wave-instruction
+  auto stage_async = [&](int pc, int bf) {
+    const int ch = pc / nfc, fc = pc - ch * nfc;
+    const int nb = min(WIDE_KC, kp - ch * WIDE_KC) / 32;
+    const int ns = min(WIDE_FW, dp - fc * WIDE_FW) / 16;
+    char* dHi = smem + (size_t)bf * WIDE_BUF;
+    for (int q = wave; q < NBW * NSW; q += WIDE_WAVES) {
+      const int blk = q / NSW, t = q - blk * NSW;
+      if (blk >= nb || t >= ns) continue;
+      const size_t src = ((size_t)(ch * WIDE_KC + blk * 32 + r) * dp + fc * WIDE_FW + 16 * t + 8 * h) * 2;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(A.Chi) + src,
+                                       (__attribute__((address_space(3))) void*)(dHi + (size_t)q * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(A.Clo) + src,
+                                       (__attribute__((address_space(3))) void*)(dHi + HIMG + (size_t)q * 1024), 16,
+                                       0, 0);
     }
-    if (fc == 0)
-      for (int id = threadIdx.x; id < nb * 32; id += 256) sCn[id] = A.cn2s[(size_t)ch * WIDE_KC + id];
+    if (fc == 0 && wave == WIDE_WAVES - 1) {  // ||c||^2 s^2 of the chunk: nb * 128 bytes
+      const char* gc = reinterpret_cast<const char*>(A.cn2s + (size_t)ch * WIDE_KC);
+      if (lane * 16 < nb * 128)
+        __builtin_amdgcn_global_load_lds(gc + lane * 16, (__attribute__((address_space(3))) void*)(dHi + 2 * HIMG),
+                                         16, 0, 0);
+    }
   };
 
-  const uint32_t gw = blockIdx.x * 4 + wave;
+  const uint32_t gw = blockIdx.x * WIDE_WAVES + wave;
   QEntry* wq = A.queue + (size_t)gw * A.seg;
   uint32_t qn = 0, qf = 0;
-  const char* laneHi = sHi + lane * 16;
-  const char* laneLo = sLo + lane * 16;
-  const float* laneCn = sCn + 4 * h;
+  int cbuf = 0;
+  if ((int64_t)blockIdx.x < nwt) stage_async(0, 0);
 
   // every wave of the workgroup runs the same trip counts (barriers inside);
   // a tile past the end computes on row n - 1 and is dropped at the end
   for (int64_t wt = blockIdx.x; wt < nwt; wt += gridDim.x) {
-    const int64_t tile = wt * 4 + wave;
+    const int64_t tile = wt * WIDE_WAVES + wave;
     const int64_t row = tile * 32 + r;
     const bool valid = row < n;
     const float* xr = A.X + (valid ? row : (n - 1)) * dp + 8 * h;
@@ -1041,59 +1048,78 @@ __global__ __launch_bounds__(256, 1) void k_assign_wide(MfmaArgs A, int dp) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) a1[c] = a2[c] = a3[c] = FLT_MAX;
     float xx = 0.0f;
-    for (int ch = 0; ch < nkc; ++ch) {
-      const int nb = min(WIDE_KC, kp - ch * WIDE_KC) / 32;  // 2 or 4 (kp a multiple of 64)
-      f32x16 acc[NBW];
-      for (int fc = 0; fc < nfc; ++fc) {
-        const int ns = min(WIDE_FW, dp - fc * WIDE_FW) / 16;
-        __syncthreads();  // the previous piece is consumed
-        stage(ch, fc, nb, ns);
-        __syncthreads();
-        if (fc == 0) {
+    // this row's slice of the next piece's features (lane (r, h): 8 per K-step)
+    float4 xv[NSW][2];
+    auto load_x = [&](int fc) {
+      const int ns = min(WIDE_FW, dp - fc * WIDE_FW) / 16;
 #pragma unroll
-          for (int blk = 0; blk < NBW; ++blk)
+      for (int t = 0; t < NSW; ++t) {
+        if (t >= ns) continue;
+        xv[t][0] = *reinterpret_cast<const float4*>(xr + fc * WIDE_FW + 16 * t);
+        xv[t][1] = *reinterpret_cast<const float4*>(xr + fc * WIDE_FW + 16 * t + 4);
+      }
+    };
+    load_x(0);
+    f32x16 acc[NBW];
+    for (int pc = 0; pc < npc; ++pc) {
+      const int ch = pc / nfc, fc = pc - ch * nfc;
+      const int nb = min(WIDE_KC, kp - ch * WIDE_KC) / 32;  // even: kp is a multiple of 64
+      const int ns = min(WIDE_FW, dp - fc * WIDE_FW) / 16;
+      // this piece's DMA (and the row slice) landed; the other buffer is free
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const char* laneHi = smem + (size_t)cbuf * WIDE_BUF + lane * 16;
+      const char* laneLo = laneHi + HIMG;
+      const float* laneCn = reinterpret_cast<const float*>(smem + (size_t)cbuf * WIDE_BUF + 2 * HIMG) + 4 * h;
+      if (pc + 1 < npc)
+        stage_async(pc + 1, cbuf ^ 1);
+      else if (wt + gridDim.x < nwt)
+        stage_async(0, cbuf ^ 1);  // the next tile group starts over at piece 0
+      cbuf ^= 1;
+      // B operand: lane (r, h) holds features [16t + 8h, 16t + 8h + 8) of the piece
+      f16x8 bh[NSW], bl[NSW];
 #pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-              const float4 cv = *reinterpret_cast<const float4*>(laneCn + blk * 32 + 8 * g4);
-              acc[blk][4 * g4 + 0] = cv.x;
-              acc[blk][4 * g4 + 1] = cv.y;
-              acc[blk][4 * g4 + 2] = cv.z;
-              acc[blk][4 * g4 + 3] = cv.w;
-            }
-        }
-        // B operand: lane (r, h) holds features [16t + 8h, 16t + 8h + 8) of the chunk
-        f16x8 bh[NSW], bl[NSW];
+      for (int t = 0; t < NSW; ++t) {
+        const float e8[8] = {xv[t][0].x, xv[t][0].y, xv[t][0].z, xv[t][0].w,
+                             xv[t][1].x, xv[t][1].y, xv[t][1].z, xv[t][1].w};
 #pragma unroll
-        for (int t = 0; t < NSW; ++t) {
-          if (t >= ns) continue;  // (not break: the loop must unroll fully)
-          const float4 v0 = *reinterpret_cast<const float4*>(xr + fc * WIDE_FW + 16 * t);
-          const float4 v1 = *reinterpret_cast<const float4*>(xr + fc * WIDE_FW + 16 * t + 4);
-          const float xv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float xs = xv[e] * s;
-            const _Float16 hi = (_Float16)xs;
-            bh[t][e] = hi;
-            bl[t][e] = (_Float16)(xs - (float)hi);
-            if (ch == 0) xx = fmaf(xs, xs, xx);
-          }
-        }
-#pragma unroll
-        for (int t = 0; t < NSW; ++t) {
-          if (t >= ns) continue;
-#pragma unroll
-          for (int blk = 0; blk < NBW; ++blk) {
-            if (blk >= nb) continue;
-            const size_t off = (size_t)blk * BLKB + (size_t)t * 1024;
-            const f16x8 fh = *reinterpret_cast<const f16x8*>(laneHi + off);
-            const f16x8 fl = *reinterpret_cast<const f16x8*>(laneLo + off);
-            acc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh, bl[t], acc[blk], 0, 0, 0);
-            acc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fl, bh[t], acc[blk], 0, 0, 0);
-            acc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh, bh[t], acc[blk], 0, 0, 0);
-          }
+        for (int e = 0; e < 8; ++e) {
+          const float xs = (t < ns) ? e8[e] * s : 0.0f;
+          const _Float16 hi = (_Float16)xs;
+          bh[t][e] = hi;
+          bl[t][e] = (_Float16)(xs - (float)hi);
+          if (ch == 0) xx = fmaf(xs, xs, xx);
         }
       }
-      // register reg of block blk holds centroid j = 32 (4 ch + blk) + 4h +
+      if (pc + 1 < npc) load_x(fc + 1 < nfc ? fc + 1 : 0);  // one piece ahead
+      if (fc == 0) {
+#pragma unroll
+        for (int blk = 0; blk < NBW; ++blk)
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const float4 cv = *reinterpret_cast<const float4*>(laneCn + blk * 32 + 8 * g4);
+            acc[blk][4 * g4 + 0] = cv.x;
+            acc[blk][4 * g4 + 1] = cv.y;
+            acc[blk][4 * g4 + 2] = cv.z;
+            acc[blk][4 * g4 + 3] = cv.w;
+          }
+      }
+#pragma unroll
+      for (int t = 0; t < NSW; ++t) {
+        if (t >= ns) continue;
+#pragma unroll
+        for (int blk = 0; blk < NBW; ++blk) {
+          if (blk >= nb) continue;
+          const size_t off = (size_t)(blk * NSW + t) * 1024;
+          const f16x8 fh = *reinterpret_cast<const f16x8*>(laneHi + off);
+          const f16x8 fl = *reinterpret_cast<const f16x8*>(laneLo + off);
+          acc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh, bl[t], acc[blk], 0, 0, 0);
+          acc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fl, bh[t], acc[blk], 0, 0, 0);
+          acc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh, bh[t], acc[blk], 0, 0, 0);
+        }
+      }
+      if (fc + 1 < nfc) continue;
+      // register reg of block blk holds centroid j = 32 (NBW ch + blk) + 4h +
       // (reg & 3) + 8 (reg >> 2); chain reg & 3 keeps j >> 2 in the key
 #pragma unroll
       for (int blk = 0; blk < NBW; ++blk) {
@@ -1273,15 +1299,14 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
   if (g.dp > 256) {
-    const int64_t nwt = ((g.n + 31) / 32 + 3) / 4;
-    const int nb = (int)(nwt < n_cu ? nwt : n_cu);
+    const int64_t nwt = ((g.n + 31) / 32 + WIDE_WAVES - 1) / WIDE_WAVES;
+    const int nb = (int)(nwt < n_cu ? nwt : n_cu);  // one workgroup per CU (2 x 65 KiB of LDS)
     const uint32_t seg = (uint32_t)(((nwt + nb - 1) / nb) * 32);
     ql->seg = seg;
-    ql->nwaves = (uint32_t)(nb * 4);
+    ql->nwaves = (uint32_t)(nb * WIDE_WAVES);
     MfmaArgs a{X, g.n, g.k, g.kp, WIDE_KC, seg, Chi, Clo, cn2s, cmax, xabs, cabs, labels, queue, qcount, gate,
                nullptr, nullptr, 0};
-    const size_t lds = 2 * (size_t)WIDE_KC * WIDE_FW * 2 + (size_t)WIDE_KC * 4;
-    hipLaunchKernelGGL(k_assign_wide, dim3(nb), dim3(256), lds, s, a, g.dp);
+    hipLaunchKernelGGL(k_assign_wide, dim3(nb), dim3(WIDE_WAVES * 64), 2 * WIDE_BUF, s, a, g.dp);
     return hipGetLastError();
   }
   int waves = 8;

@@ -152,9 +152,9 @@ def _check_labels(X, C, labels):
     (4000, 40, 300, 30),       # dp 48 unfused: k_stats lane groups of 12 (4 lanes idle)
     (4000, 90, 200, 30),       # dp 96 unfused: lane groups of 24
     (3000, 180, 150, 30),      # dp 192 unfused: lane groups of 48
-    (6000, 300, 70, 20),       # d=300 -> 304: feature-chunked screen (k_assign_wide), one centroid chunk
-    (3000, 784, 200, 40),      # d=784: 2 centroid x 4 feature chunks, statistics over 196-wide ranges
-    (2000, 300, 700, 50),      # wide rows, 6 centroid chunks, 3 cluster ranges
+    (6000, 300, 70, 20),       # d=300 -> 304: feature-piece screen (k_assign_wide), one centroid chunk, last piece 48 wide
+    (3000, 784, 200, 40),      # d=784: 13 feature pieces (last one 16 wide), statistics over 196-wide ranges
+    (2000, 300, 700, 50),      # wide rows, 3 centroid chunks (the last 192 wide), 3 cluster ranges
 ])
 def test_one_step_vs_oracle(n, d, k, centers):
     X = _blobs(n, d, centers, seed=n + d + k)
