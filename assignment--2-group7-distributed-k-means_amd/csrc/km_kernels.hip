@@ -977,7 +977,10 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
 // Keys, chains, the rigorous bound and the queue are those of k_assign_mfma
 // (top-3 chains).  X is read once per centroid chunk (once for k <= 256).
 // ---------------------------------------------------------------------------
-static constexpr int WIDE_KC = 256, WIDE_FW = 64, WIDE_WAVES = 8;
+#ifndef KM_WIDE_FW
+#define KM_WIDE_FW 64
+#endif
+static constexpr int WIDE_KC = 256, WIDE_FW = KM_WIDE_FW, WIDE_WAVES = 8;
 static constexpr int WIDE_MAX_DP = 2048;  // k_fullscan stages 2 x 8 rows in LDS
 static constexpr size_t WIDE_BUF = 2 * (size_t)(WIDE_KC / 32) * (WIDE_FW / 16) * 1024 + WIDE_KC * 4;
 
