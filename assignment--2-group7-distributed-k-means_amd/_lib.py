@@ -13,7 +13,10 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libkmeans_amd.so")
+# KM_LIB: another build of the same sources (the diagnostic library, or an A/B
+# variant from `make alt`), selected per process instead of copied over the
+# product file (scripts/gpu_ab.sh)
+LIB_PATH = os.environ.get("KM_LIB") or os.path.join(HERE, "libkmeans_amd.so")
 ROOT = os.path.dirname(HERE)
 HEADER = os.path.join(ROOT, "include", "kmeans_amd.h")
 

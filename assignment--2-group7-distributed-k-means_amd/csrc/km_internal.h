@@ -119,8 +119,11 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
                         double* stats, int with_stats, int mode, int n_cu, QLayout* ql, const int* gate,
                         hipStream_t s, const float* C32, const float* cmax, float* bal, const double* C64P,
                         double* sse);
-hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float* cabs, int dp, float* bnd,
+// bound constants of the fused screen (the MFMA shape it runs on: fused16_ok)
+hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float* cabs, const Geometry& g, float* bnd,
                                const int* gate, hipStream_t s);
+// the fused screen runs on v_mfma_f32_16x16x32_f16 (k_fused16) for this geometry
+bool fused16_ok(const Geometry& g);
 hipError_t launch_row_norm(const float* X, const Geometry& g, float* xnorm, hipStream_t s);
 // large k: counting sort of the labels + per-cluster float64 row sums (X read
 // once); scratch = sorted_stats_words(n, k) uint32 words

@@ -77,14 +77,31 @@ __device__ inline float wave_sum_f(float v) {
 //       group's maximum are dropped; worst observed U|D| + 3.7 u max|term|)
 //   fp16 underflow: u sqrt(dp) (xn + 2 cm)
 // times a 1.5 safety factor.
-// B0 = screen_slope * xn_s + screen_icpt (affine in xn_s)
-__host__ __device__ inline float screen_slope(float cm_s, int dp) {
-  const float nm = 3.0f * (float)dp / 16.0f;  // MFMAs per block chain
-  return 1.5f * ((6.5f * 2.384185791015625e-07f + 0.5f * U24) * cm_s + nm * 2.0f * U24 * cm_s + U24 * sqrtf((float)dp));
+// The same terms for v_mfma_f32_16x16x32_f16 (k_fused16; characterised in
+// scripts/probes/mfma_align16.hip): its 32 products form four 8-product
+// groups, each aligned to its own maximum (terms > 25 bits below it dropped,
+// <= 7 u per group and max product), and the four group sums enter the
+// accumulator one after the other, each rounded (a group sum 24 bits below
+// the running value is lost, one above it is exact).  Per MFMA: <= 4
+// roundings of a partial sum bounded like |D| and 28 u max|product|; a block
+// chain has 3 dp/32 of them.  In units of the 32x32x16 model: nr = rounding
+// terms per chain, nt = truncation terms (28 u * 2 pm each).
+struct ChainErr {
+  float nr, nt;
+};
+__host__ __device__ inline ChainErr chain_err(int dp, int shape16) {
+  const float nm32 = 3.0f * (float)dp / 16.0f;  // 32x32x16 MFMAs per block chain
+  return shape16 ? ChainErr{2.0f * nm32, nm32} : ChainErr{nm32, nm32};
 }
-__host__ __device__ inline float screen_icpt(float cm_s, float pm_s, int dp) {
-  const float nm = 3.0f * (float)dp / 16.0f;
-  return 1.5f * (U24 * cm_s * cm_s + nm * (U24 * cm_s * cm_s + 28.0f * U24 * pm_s) +
+// B0 = screen_slope * xn_s + screen_icpt (affine in xn_s)
+__host__ __device__ inline float screen_slope(float cm_s, int dp, int shape16 = 0) {
+  const ChainErr ce = chain_err(dp, shape16);
+  return 1.5f * ((6.5f * 2.384185791015625e-07f + 0.5f * U24) * cm_s + ce.nr * 2.0f * U24 * cm_s +
+                 U24 * sqrtf((float)dp));
+}
+__host__ __device__ inline float screen_icpt(float cm_s, float pm_s, int dp, int shape16 = 0) {
+  const ChainErr ce = chain_err(dp, shape16);
+  return 1.5f * (U24 * cm_s * cm_s + ce.nr * U24 * cm_s * cm_s + ce.nt * 28.0f * U24 * pm_s +
                  2.0f * U24 * sqrtf((float)dp) * cm_s);
 }
 __host__ __device__ inline float screen_b0(float xn_s, float cm_s, float pm_s, int dp) {
@@ -129,13 +146,13 @@ struct KeyBounds {
 
 // E(r) coefficients for a point of scaled norm bound xn_s (xabs_s: scaled
 // max |x_f| over the data), the terms of screen_b0 with the same 1.5 safety
-__device__ __forceinline__ KeyBounds key_bounds(float xn_s, float xabs_s, int dp, float rho) {
-  const float nm = 3.0f * (float)dp / 16.0f;
+__device__ __forceinline__ KeyBounds key_bounds(float xn_s, float xabs_s, int dp, float rho, int shape16 = 0) {
+  const ChainErr ce = chain_err(dp, shape16);
   const float sq = sqrtf((float)dp);
   KeyBounds kb;
-  kb.e2 = 1.5f * U24 * (1.0f + nm);
-  kb.e1 = 1.5f * ((6.5f * 2.384185791015625e-07f + 0.5f * U24 + 2.0f * nm * U24) * xn_s +
-                  28.0f * nm * U24 * fminf(xn_s, xabs_s) + 2.0f * U24 * sq);
+  kb.e2 = 1.5f * U24 * (1.0f + ce.nr);
+  kb.e1 = 1.5f * ((6.5f * 2.384185791015625e-07f + 0.5f * U24 + 2.0f * ce.nr * U24) * xn_s +
+                  28.0f * ce.nt * U24 * fminf(xn_s, xabs_s) + 2.0f * U24 * sq);
   kb.e0 = 1.5f * U24 * sq * xn_s;
   kb.x = xn_s;
   kb.rho = rho * 1.01f + 2.0f * U24;
@@ -1864,6 +1881,436 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// k_fused16: k_fused on v_mfma_f32_16x16x32_f16 ("MFMA
+// shape").  Same output tile per wave -- 32 rows x KP centroids per tile,
+// fp16x3 scores, images in AGPRs, rows double-buffered in registers -- with
+// 16x16 accumulators: a block of 32 centroids is two 16-centroid halves (cb)
+// times two 16-row groups (pg), 12 NS2 MFMAs of 16 cycles (k_fused: 3 NS of
+// 32).  Lane l, q = l >> 4:
+//   A operand: centroid 32 b + 16 cb + (l & 15), features 32 s + 8 q .. + 8
+//              (image piece (2 b + cb) NS2 + s, k_frag_images16);
+//   B operand: row 16 pg + (l & 15), the same features;
+//   register i of accumulator (cb, pg): centroid j = 32 b + 16 cb + 4 q + i.
+// Chains are (j & 3, q): 16 per row (k_fused: 8); keys carry j >> 2.  After
+// the blocks the two row groups are reduce-scattered over the lane halves
+// (lanes 0-31 keep group 0, 32-63 group 1) and merged over quarter pairs, so
+// lanes l and l ^ 16 hold the top-3 and best two of row (l & 15) + 16 (l >> 5).
+// The bound is screen_b0's with the 16x16x32 accumulation model (chain_err).
+// ---------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// KM_SWAP_ASM: the swaps as inline asm with two wait states on both sides
+// (A/B of the builtin's code generation)
+#ifndef KM_SWAP_ASM
+#define KM_SWAP_ASM 0
+#endif
+__device__ __forceinline__ void perm_quarters(uint32_t v, uint32_t& lo, uint32_t& hi) {
+  // lo = value of lane (l & ~16), hi = value of lane (l | 16), in every lane
+#if KM_SWAP_ASM
+  lo = v;
+  hi = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(lo), "+v"(hi));
+#else
+  const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  lo = p[0];
+  hi = p[1];
+#endif
+}
+
+template <int NS2, int NB, bool STATS, bool REF = true, bool SSE = false>
+__global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
+  if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
+  constexpr int DP = 32 * NS2;
+  constexpr int KP = 32 * NB;
+  constexpr int WAVES = 4;
+  constexpr int B = ceil_log2_c(KP);
+  static_assert(B >= 3 && B - 2 <= 12, "index bits");
+  static_assert(NB >= 2, "pipelined blocks");
+  constexpr uint32_t maskq = (1u << (B - 2)) - 1u;
+  constexpr int TS = KP;
+  constexpr int NMF = 12 * NS2;  // MFMAs per block
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* sCn = reinterpret_cast<float*>(smem);            // ||c||^2 s^2 [KP]
+  double* tab = reinterpret_cast<double*>(smem + KP * 4);  // [DP + 1][TS]
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int c16 = lane & 15;
+  const int q = lane >> 4;
+  const int prow = c16 + 16 * (lane >> 5);  // the tile row this lane owns after the merge
+  for (int i = threadIdx.x; i < KP; i += WAVES * 64) sCn[i] = A.cn2s[i];
+  if constexpr (STATS)
+    for (int i = threadIdx.x; i < (DP + 1) * TS; i += WAVES * 64) tab[i] = 0.0;
+  f16x8 Ahi[NB][2][NS2], Alo[NB][2][NS2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int t = 0; t < NS2; ++t) {
+        Ahi[b][cb][t] = __builtin_bit_cast(f16x8, A.ChiF[((2 * b + cb) * NS2 + t) * 64 + lane]);
+        Alo[b][cb][t] = __builtin_bit_cast(f16x8, A.CloF[((2 * b + cb) * NS2 + t) * 64 + lane]);
+      }
+  // consume the image loads before the loop (see k_fused)
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int t = 0; t < NS2; ++t) asm volatile("" : "+a"(Ahi[b][cb][t]), "+a"(Alo[b][cb][t]));
+  __syncthreads();
+
+  const float s = mfma_scale(*A.xabs, *A.cabs);
+  const float alpha = A.bnd[0], beta = A.bnd[1];
+  const float rho = __builtin_ldexpf(1.0f, B - 2 - 23) * 1.01f;
+  const int64_t n = A.n;
+  const int64_t ntiles = (n + 31) / 32;
+  const uint32_t gw = blockIdx.x * WAVES + wave;
+  QEntry* wq = A.queue + (size_t)gw * A.seg;
+  uint32_t qn = 0, qf = 0;
+  const int64_t tstride = (int64_t)gridDim.x * WAVES;
+  const float4* cnl = reinterpret_cast<const float4*>(sCn + 4 * q);  // + 8 blk + 4 cb
+
+  auto load_tile = [&](int64_t tile, float4 (&xq)[2][NS2][2], float& xnq) {
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg) {
+      const int64_t row = tile * 32 + 16 * pg + c16;
+      const int64_t rr = row < n ? row : (n - 1);
+      const float* xr = A.X + rr * DP + 8 * q;
+#pragma unroll
+      for (int t = 0; t < NS2; ++t) {
+        xq[pg][t][0] = *reinterpret_cast<const float4*>(xr + 32 * t);
+        xq[pg][t][1] = *reinterpret_cast<const float4*>(xr + 32 * t + 4);
+      }
+    }
+    const int64_t orow = tile * 32 + prow;
+    xnq = A.xnorm[orow < n ? orow : (n - 1)];
+  };
+
+  double ss_acc = 0.0;  // SSE variant: this lane's residual sum
+  auto process_tile = [&](int64_t tile, const float4 (&xc)[2][NS2][2], float xn) {
+    const int64_t row = tile * 32 + prow;
+    const bool valid = row < n;
+    // B operands: xs = hi + lo (fp16, RN), as in k_fused
+    f16x8 bh[2][NS2], bl[2][NS2];
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg)
+#pragma unroll
+      for (int t = 0; t < NS2; ++t) {
+        const float xv[8] = {xc[pg][t][0].x, xc[pg][t][0].y, xc[pg][t][0].z, xc[pg][t][0].w,
+                             xc[pg][t][1].x, xc[pg][t][1].y, xc[pg][t][1].z, xc[pg][t][1].w};
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const float xs0 = xv[e] * s, xs1 = xv[e + 1] * s;
+          const f16x2 hp = {(_Float16)xs0, (_Float16)xs1};
+#if KM_SPLIT_ASM
+          uint32_t lp;
+          asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
+              "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+              : "=&v"(lp)
+              : "v"(__builtin_bit_cast(uint32_t, hp)), "v"(xs0), "v"(xs1));
+          const f16x2 lo = __builtin_bit_cast(f16x2, lp);
+#else
+          // xs - hi is exact in fp32: the same bits as the fused mix form
+          const f16x2 lo = {(_Float16)(xs0 - (float)hp[0]), (_Float16)(xs1 - (float)hp[1])};
+#endif
+          bh[pg][t][e] = hp[0];
+          bh[pg][t][e + 1] = hp[1];
+          bl[pg][t][e] = lo[0];
+          bl[pg][t][e + 1] = lo[1];
+        }
+      }
+    float a1[2][4], a2[2][4];
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) a1[pg][c] = a2[pg][c] = FLT_MAX;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int t = 0; t < NS2; ++t) asm volatile("" : "+a"(Ahi[b][cb][t]), "+a"(Alo[b][cb][t]));
+    struct Acc {
+      f32x4 v[2][2];  // [cb][pg]
+    };
+    auto cn_init = [&](int blk, int cb) {
+      const float4 cv = cnl[8 * blk + 4 * cb];
+      f32x4 r = {cv.x, cv.y, cv.z, cv.w};
+      return r;
+    };
+    auto mfma_block = [&](const f32x4 (&ini)[2], int blk) {
+      Acc a;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int pg = 0; pg < 2; ++pg) a.v[cb][pg] = ini[cb];
+#pragma unroll
+      for (int t = 0; t < NS2; ++t) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int pg = 0; pg < 2; ++pg)
+            a.v[cb][pg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ahi[blk][cb][t], bl[pg][t], a.v[cb][pg], 0, 0, 0);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int pg = 0; pg < 2; ++pg)
+            a.v[cb][pg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Alo[blk][cb][t], bh[pg][t], a.v[cb][pg], 0, 0, 0);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int pg = 0; pg < 2; ++pg)
+            a.v[cb][pg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ahi[blk][cb][t], bh[pg][t], a.v[cb][pg], 0, 0, 0);
+      }
+      return a;
+    };
+    // chain (c, q) of row group pg keeps its top two keys; the two halves cb
+    // of a block are folded in together (5 VALU per 2 scores, as k_fused)
+    auto keys_block = [&](const Acc& a, int blk) {
+      const uint32_t j0 = (uint32_t)(8 * blk + q), j1 = j0 + 4u;  // j >> 2 of halves 0 and 1
+#pragma unroll
+      for (int pg = 0; pg < 2; ++pg)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float ka = __uint_as_float((__float_as_uint(a.v[0][pg][c]) & ~maskq) | j0);
+          const float kb = __uint_as_float((__float_as_uint(a.v[1][pg][c]) & ~maskq) | j1);
+          const float t = __builtin_amdgcn_fmed3f(a1[pg][c], ka, kb);
+          a1[pg][c] = __builtin_fminf(__builtin_fminf(a1[pg][c], ka), kb);
+          a2[pg][c] = __builtin_fminf(a2[pg][c], t);
+        }
+    };
+    // software pipeline as in k_fused: block blk's MFMAs overlap block blk-1's
+    // key updates; block blk+1's accumulator init is read from LDS meanwhile
+    Acc accs[2];
+    f32x4 nxt[2] = {cn_init(1, 0), cn_init(1, 1)};
+    {
+      const f32x4 ini[2] = {cn_init(0, 0), cn_init(0, 1)};
+      accs[0] = mfma_block(ini, 0);
+    }
+#pragma unroll
+    for (int blk = 1; blk < NB; ++blk) {
+      const f32x4 cin[2] = {nxt[0], nxt[1]};
+      if (blk + 1 < NB) {
+        nxt[0] = cn_init(blk + 1, 0);
+        nxt[1] = cn_init(blk + 1, 1);
+      }
+      accs[blk & 1] = mfma_block(cin, blk);
+      keys_block(accs[(blk - 1) & 1], blk - 1);
+      // MFMA, next block's init reads, MFMA, then (VALU x m, MFMA) pairs
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+#pragma unroll
+      for (int i = 0; i < NMF - 2; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x2, 48 / (NMF - 2) + 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    keys_block(accs[(NB - 1) & 1], NB - 1);
+
+    // per row group: the four chains of this lane merged (as k_fused)
+    auto pidx = [&](float key, int c) { return ((__float_as_uint(key) & maskq) << 2) | (uint32_t)c; };
+    float g1[2], g2[2], g3[2];
+    uint32_t gp1[2], gp2[2];
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg) {
+      float k1 = a1[pg][0], k2 = a2[pg][0], k3 = a2[pg][0];
+      uint32_t p1 = pidx(a1[pg][0], 0), p2 = pidx(a2[pg][0], 0);
+      float m1 = a1[pg][2], m2 = a2[pg][2], m3 = a2[pg][2];
+      uint32_t q1 = pidx(a1[pg][2], 2), q2 = pidx(a2[pg][2], 2);
+      merge3(k1, k2, k3, p1, p2, a1[pg][1], a2[pg][1], a2[pg][1], pidx(a1[pg][1], 1), pidx(a2[pg][1], 1));
+      merge3(m1, m2, m3, q1, q2, a1[pg][3], a2[pg][3], a2[pg][3], pidx(a1[pg][3], 3), pidx(a2[pg][3], 3));
+      merge3(k1, k2, k3, p1, p2, m1, m2, m3, q1, q2);
+      g1[pg] = k1;
+      g2[pg] = k2;
+      g3[pg] = k3;
+      gp1[pg] = p1;
+      gp2[pg] = p2;
+    }
+    // reduce-scatter over the lane halves: permlane32_swap(group 0, group 1)
+    // gives lanes 0-31 group 0 of lanes l and l + 32, lanes 32-63 group 1 of
+    // lanes l - 32 and l (the lower lane's side first in both)
+    auto swap_groups = [](uint32_t v0, uint32_t v1, uint32_t& lo, uint32_t& hi) {
+#if KM_SWAP_ASM
+      lo = v0;
+      hi = v1;
+      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(lo), "+v"(hi));
+#else
+      const auto p = __builtin_amdgcn_permlane32_swap(v0, v1, false, false);
+      lo = p[0];
+      hi = p[1];
+#endif
+    };
+    float k1, k2, k3;
+    uint32_t p1, p2;
+    {
+      uint32_t K1, Q1, K2, Q2, K3, Q3, P1, R1, P2, R2;
+      swap_groups(__float_as_uint(g1[0]), __float_as_uint(g1[1]), K1, Q1);
+      swap_groups(__float_as_uint(g2[0]), __float_as_uint(g2[1]), K2, Q2);
+      swap_groups(__float_as_uint(g3[0]), __float_as_uint(g3[1]), K3, Q3);
+      swap_groups(gp1[0], gp1[1], P1, R1);
+      swap_groups(gp2[0], gp2[1], P2, R2);
+      k1 = __uint_as_float(K1);
+      k2 = __uint_as_float(K2);
+      k3 = __uint_as_float(K3);
+      p1 = P1;
+      p2 = P2;
+      merge3(k1, k2, k3, p1, p2, __uint_as_float(Q1), __uint_as_float(Q2), __uint_as_float(Q3), R1, R2);
+    }
+    {
+      uint32_t K1, Q1, K2, Q2, K3, Q3, P1, R1, P2, R2;
+      perm_quarters(__float_as_uint(k1), K1, Q1);
+      perm_quarters(__float_as_uint(k2), K2, Q2);
+      perm_quarters(__float_as_uint(k3), K3, Q3);
+      perm_quarters(p1, P1, R1);
+      perm_quarters(p2, P2, R2);
+      k1 = __uint_as_float(K1);
+      k2 = __uint_as_float(K2);
+      k3 = __uint_as_float(K3);
+      p1 = P1;
+      p2 = P2;
+      merge3(k1, k2, k3, p1, p2, __uint_as_float(Q1), __uint_as_float(Q2), __uint_as_float(Q3), R1, R2);
+    }
+    // p1, p2 in one chain (j & 15): no re-rank certificate (see k_fused)
+    const bool same_chain = ((p1 ^ p2) & 15u) == 0u;
+    const float B0 = fmaf(alpha, xn, beta);
+    const float thr2 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k2));
+    const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k3));
+    uint32_t kind = 0;
+    if (!(k2 - k1 > thr2)) kind = (same_chain || !(k3 - k1 > thr3)) ? 2u : 1u;
+    float u1 = 0.0f;
+    KeyBounds kb;
+    const bool refine = REF && __ballot(kind != 0u) != 0ull;
+    if (refine) {
+      kb = key_bounds(xn * s, *A.xabs * s, DP, rho, 1);
+      if (kind != 0u) {
+        u1 = kb.upper(k1);
+        if (u1 < kb.lower(k2))
+          kind = 0u;
+        else if (kind == 2u && !same_chain && kb.lower(k3) > u1)
+          kind = 1u;
+      }
+    }
+    // p1, p2 in one chain, every other chain's best separated from k1: the
+    // answer lies in chain p1 & 15, a subset of the resolver's kind-3 scan
+    // (j & 7 == p1 & 7)
+    if (__ballot(kind == 2u && same_chain) != 0ull) {
+      const uint32_t cs = p1 & 15u;
+      float o = FLT_MAX;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t h0, h1, v0, v1, v2, v3;  // chain (c, quarter 0..3) of this lane's row group
+        swap_groups(__float_as_uint(a1[0][c]), __float_as_uint(a1[1][c]), h0, h1);
+        perm_quarters(h0, v0, v1);
+        perm_quarters(h1, v2, v3);
+        if ((uint32_t)c != cs) o = kmin(o, __uint_as_float(v0));
+        if ((uint32_t)(4 + c) != cs) o = kmin(o, __uint_as_float(v1));
+        if ((uint32_t)(8 + c) != cs) o = kmin(o, __uint_as_float(v2));
+        if ((uint32_t)(12 + c) != cs) o = kmin(o, __uint_as_float(v3));
+      }
+      const float thr3x = 2.0f * B0 + rho * (fabsf(k1) + fabsf(o));
+      if (kind == 2u && same_chain && (o - k1 > thr3x || (REF && kb.lower(o) > u1))) kind = 3u;
+    }
+    const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
+    const bool lead = (q & 1) == 0;  // one lane of each pair (l, l ^ 16) writes
+    if (lead && valid) A.labels[row] = lab;
+    const bool enq = lead && valid && (kind != 0);
+    const uint64_t m = __ballot(enq);
+    if (m) {
+      const uint64_t m1 = __ballot(enq && kind == 1);
+      const uint64_t m2 = m & ~m1;
+      const uint64_t below = (1ull << lane) - 1ull;
+      if (enq) {
+        QEntry qe;
+        qe.row = (uint32_t)row;
+        qe.i1 = p1;
+        qe.i2 = p2;
+        qe.kind = kind;
+        const uint32_t pos = (kind == 1) ? qn + (uint32_t)__popcll(m1 & below)
+                                         : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
+        wq[pos] = qe;
+      }
+      qn += (uint32_t)__popcll(m1);
+      qf += (uint32_t)__popcll(m2);
+    }
+    if constexpr (STATS) {
+      // every lane holds features 32 t + 8 q .. + 8 of both row groups: the
+      // label of each decided row from its owner lanes (l & 31 and l | 32)
+      const uint32_t own = (valid && kind == 0) ? (uint32_t)lab : 0xffffffffu;
+      uint32_t li[2];
+      perm_halves(own, li[0], li[1]);
+#pragma unroll
+      for (int pg = 0; pg < 2; ++pg) {
+        if (li[pg] != 0xffffffffu) {
+          double* tp = tab + (size_t)(8 * q) * TS + li[pg];
+#pragma unroll
+          for (int t = 0; t < NS2; ++t) {
+            const float4 v0 = xc[pg][t][0], v1 = xc[pg][t][1];
+            const float xe[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) atomicAdd(tp + (size_t)(32 * t + e) * TS, (double)xe[e]);
+          }
+          if (q == 0) atomicAdd(tab + (size_t)DP * TS + li[pg], 1.0);  // count row
+          if constexpr (SSE) {
+            const double* cr = A.C64P + (size_t)li[pg] * DP + 8 * q;
+#pragma unroll
+            for (int t = 0; t < NS2; ++t) {
+              const double4 ca = *reinterpret_cast<const double4*>(cr + 32 * t);
+              const double4 cb = *reinterpret_cast<const double4*>(cr + 32 * t + 4);
+              const float4 v0 = xc[pg][t][0], v1 = xc[pg][t][1];
+              const double r0 = (double)v0.x - ca.x, r1 = (double)v0.y - ca.y;
+              const double r2 = (double)v0.z - ca.z, r3 = (double)v0.w - ca.w;
+              const double r4 = (double)v1.x - cb.x, r5 = (double)v1.y - cb.y;
+              const double r6 = (double)v1.z - cb.z, r7 = (double)v1.w - cb.w;
+              ss_acc = fma(r0, r0, ss_acc);
+              ss_acc = fma(r1, r1, ss_acc);
+              ss_acc = fma(r2, r2, ss_acc);
+              ss_acc = fma(r3, r3, ss_acc);
+              ss_acc = fma(r4, r4, ss_acc);
+              ss_acc = fma(r5, r5, ss_acc);
+              ss_acc = fma(r6, r6, ss_acc);
+              ss_acc = fma(r7, r7, ss_acc);
+            }
+          }
+        }
+      }
+    }
+  };
+
+  float4 xb0[2][NS2][2], xb1[2][NS2][2];
+  float xn0 = 0.0f, xn1 = 0.0f;
+  load_tile(gw, xb0, xn0);
+  for (int64_t tile = gw; tile < ntiles; tile += 2 * tstride) {
+    const int64_t t1 = tile + tstride;
+    load_tile(t1, xb1, xn1);
+    process_tile(tile, xb0, xn0);
+    if (t1 >= ntiles) break;
+    load_tile(t1 + tstride, xb0, xn0);
+    process_tile(t1, xb1, xn1);
+  }
+  if (lane == 0) {
+    A.qcount[2 * gw] = qn;
+    A.qcount[2 * gw + 1] = qf;
+  }
+  if constexpr (SSE) {
+    ss_acc = wave_sum(ss_acc);
+    if (lane == 0 && ss_acc != 0.0) atomicAdd(A.sse, ss_acc);
+  }
+  if constexpr (STATS) {
+    __syncthreads();
+    const int d1 = A.d + 1;
+    for (int i = threadIdx.x; i < (DP + 1) * KP; i += WAVES * 64) {
+      const int j = i / (DP + 1);
+      const int f = i - j * (DP + 1);
+      const double v = tab[(size_t)f * TS + j];
+      if (v != 0.0 && (f < A.d || f == DP) && j < A.k) atomicAdd(A.stats + (size_t)j * d1 + (f == DP ? A.d : f), v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Software-pipelined fused kernel (the c3 class with statistics, no SSE): the
 // same screen, bound, labels, queue and float64 sums as k_fused, arranged so
 // that one wave per SIMD keeps the matrix pipe busy.  In k_fused a tile's
@@ -2789,16 +3236,36 @@ __global__ __launch_bounds__(256) void k_frag_images(const _Float16* __restrict_
   CloF[id] = *reinterpret_cast<const uint4*>(Clo + src);
 }
 
+// the same for k_fused16: piece (h, t) (h = 2 b + cb, a 16-centroid half),
+// lane l holds 8 halves of row 16 h + (l & 15), features 32 t + 8 (l >> 4) .. + 8
+__global__ __launch_bounds__(256) void k_frag_images16(const _Float16* __restrict__ Chi,
+                                                       const _Float16* __restrict__ Clo, int kp, int dp,
+                                                       uint4* __restrict__ ChiF, uint4* __restrict__ CloF,
+                                                       const int* __restrict__ gate) {
+  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
+  const int ns2 = dp / 32;
+  const int total = (kp / 16) * ns2 * 64;
+  const int id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= total) return;
+  const int l = id & 63;
+  const int ht = id >> 6;
+  const int hb = ht / ns2, t = ht - hb * ns2;
+  const size_t src = (size_t)(hb * 16 + (l & 15)) * dp + 32 * t + 8 * (l >> 4);
+  ChiF[id] = *reinterpret_cast<const uint4*>(Chi + src);
+  CloF[id] = *reinterpret_cast<const uint4*>(Clo + src);
+}
+
 // screening-bound constants: B0 = alpha * ||x|| + beta (see k_assign_mfma)
 __global__ void k_bound_consts(const float* __restrict__ cmax, const float* __restrict__ xabs,
-                               const float* __restrict__ cabs, int dp, float* __restrict__ bnd, const int* __restrict__ gate) {
+                               const float* __restrict__ cabs, int dp, int shape16, float* __restrict__ bnd,
+                               const int* __restrict__ gate) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   // screen_b0 is affine in xn_s = s ||x||: B0 = bnd[0] ||x|| + bnd[1]
   const float s = mfma_scale(*xabs, *cabs);
   const float cm = *cmax * s;
   const float pm = (*cabs * s) * (*xabs * s) * 1.0001f;
-  bnd[0] = screen_slope(cm, dp) * s * 1.0001f;  // per unscaled ||x||
-  bnd[1] = screen_icpt(cm, pm, dp) * 1.0001f;
+  bnd[0] = screen_slope(cm, dp, shape16) * s * 1.0001f;  // per unscaled ||x||
+  bnd[1] = screen_icpt(cm, pm, dp, shape16) * 1.0001f;
 }
 
 // upper bound of ||x|| per row (float64 sum, rounded up): L = dp/4 lanes per
@@ -2882,6 +3349,16 @@ bool fused_path_ok(const Geometry& g) {
 
 bool fast_path_ok(const Geometry& g) { return g.dp == 64 && g.kp == 256; }
 
+// k_fused16 (v_mfma_f32_16x16x32_f16) for dp a multiple of 32; KM_FUSED16=0
+// builds the 32x32x16 k_fused everywhere (A/B arm, make alt)
+#ifndef KM_FUSED16
+#define KM_FUSED16 0
+#endif
+bool fused16_ok(const Geometry& g) {
+  static const int on = diag_env("KM_FUSED16", KM_FUSED16);
+  return on && fused_path_ok(g) && g.dp % 32 == 0;
+}
+
 hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, const _Float16* Chi,
                         const _Float16* Clo, uint4* ChiF, uint4* CloF, const float* cn2s, const float* bnd,
                         const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,
@@ -2923,7 +3400,12 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
     return hipGetLastError();
   }
 #endif
-  {
+  const bool shape16 = fused16_ok(g);
+  if (shape16) {
+    const int total = (g.kp / 16) * (g.dp / 32) * 64;
+    hipLaunchKernelGGL(k_frag_images16, dim3((total + 255) / 256), dim3(256), 0, s, Chi, Clo, g.kp, g.dp, ChiF, CloF,
+                       gate);
+  } else {
     const int total = nb * ns * 64;
     hipLaunchKernelGGL(k_frag_images, dim3((total + 255) / 256), dim3(256), 0, s, Chi, Clo, g.kp, g.dp, ChiF, CloF, gate);
   }
@@ -2973,6 +3455,37 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
     }
   }
 #endif
+#define KM_FUSED16_CASE(NS2_, NB_)                                                                      \
+  case NS2_ * 100 + NB_:                                                                                \
+    if (with_stats && sse)                                                                              \
+      hipLaunchKernelGGL((k_fused16<NS2_, NB_, true, true, true>), dim3(nbk), dim3(256), lds, s, a);    \
+    else if (with_stats && !refine)                                                                     \
+      hipLaunchKernelGGL((k_fused16<NS2_, NB_, true, false>), dim3(nbk), dim3(256), lds, s, a);         \
+    else if (with_stats)                                                                                \
+      hipLaunchKernelGGL((k_fused16<NS2_, NB_, true>), dim3(nbk), dim3(256), lds, s, a);                \
+    else if (KM_F16_PREDICT == 1)                                                                       \
+      hipLaunchKernelGGL((k_fused16<NS2_, NB_, true>), dim3(nbk), dim3(256), lds_s, s, a);              \
+    else if (KM_F16_PREDICT == 2)                                                                       \
+      hipLaunchKernelGGL((k_fused16<NS2_, NB_, false, false>), dim3(nbk), dim3(256), lds, s, a);        \
+    else                                                                                                \
+      hipLaunchKernelGGL((k_fused16<NS2_, NB_, false>), dim3(nbk), dim3(256), lds, s, a);               \
+    break;
+#ifndef KM_F16_PREDICT
+#define KM_F16_PREDICT 0
+#endif
+  const size_t lds_s = (size_t)g.kp * 4 + (size_t)(g.dp + 1) * g.kp * 8;
+  if (shape16) {
+    switch ((g.dp / 32) * 100 + nb) {
+      KM_FUSED16_CASE(2, 2) KM_FUSED16_CASE(2, 4) KM_FUSED16_CASE(2, 6) KM_FUSED16_CASE(2, 8)
+      KM_FUSED16_CASE(1, 2) KM_FUSED16_CASE(1, 4) KM_FUSED16_CASE(1, 6) KM_FUSED16_CASE(1, 8) KM_FUSED16_CASE(1, 12)
+      KM_FUSED16_CASE(1, 16)
+      KM_FUSED16_CASE(4, 2) KM_FUSED16_CASE(4, 4)
+      default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+#undef KM_FUSED16_CASE
   switch (ns * 100 + nb) {
     KM_FUSED_CASE(4, 2) KM_FUSED_CASE(4, 4) KM_FUSED_CASE(4, 6) KM_FUSED_CASE(4, 8)
     KM_FUSED_CASE(2, 2) KM_FUSED_CASE(2, 4) KM_FUSED_CASE(2, 6) KM_FUSED_CASE(2, 8) KM_FUSED_CASE(2, 12)
@@ -2986,9 +3499,10 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
   return hipGetLastError();
 }
 
-hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float* cabs, int dp, float* bnd,
+hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float* cabs, const Geometry& g, float* bnd,
                                const int* gate, hipStream_t s) {
-  hipLaunchKernelGGL(k_bound_consts, dim3(1), dim3(1), 0, s, cmax, xabs, cabs, dp, bnd, gate);
+  hipLaunchKernelGGL(k_bound_consts, dim3(1), dim3(1), 0, s, cmax, xabs, cabs, g.dp, fused16_ok(g) ? 1 : 0, bnd,
+                     gate);
   return hipGetLastError();
 }
 

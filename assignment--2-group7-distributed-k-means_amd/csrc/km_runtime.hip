@@ -285,7 +285,7 @@ int prep(km_ctx* c, const double* src) {
   KM_HIP(km::launch_prep_centroids(src, c->g, c->C32, c->cn2, c->cmax, c->cabs, c->C64T, c->C64P, c->gate,
                                    c->stream));
   KM_HIP(km::launch_prep_split(c->C32, c->g, c->cn2, c->xabs, c->cabs, c->Chi, c->Clo, c->cn2s, c->gate, c->stream));
-  KM_HIP(km::launch_bound_consts(c->cmax, c->xabs, c->cabs, c->g.dp, c->bnd, c->gate, c->stream));
+  KM_HIP(km::launch_bound_consts(c->cmax, c->xabs, c->cabs, c->g, c->bnd, c->gate, c->stream));
   return KM_OK;
 }
 

@@ -247,6 +247,12 @@ def rank_rows(n: int, world: int, rank: int) -> Tuple[int, int]:
     return (rank * n) // world, ((rank + 1) * n) // world
 
 
+class EmptyDataset(ValueError):
+    """The dataset has no rows.  ``fit`` turns it into the reference's init
+    error (takeSample returns [] for an empty RDD, kmeans_spark.py:72-74);
+    ``predict`` returns an empty result (its lazy map over no rows)."""
+
+
 def place(rdd, comm) -> Placement:
     if isinstance(rdd, DeviceBlobs):
         a, b = rank_rows(rdd.n, comm.world, comm.rank)
@@ -256,7 +262,7 @@ def place(rdd, comm) -> Placement:
                          d=rdd.d, dtype=np.float64, blobs=rdd)
     sizes, d, dtype = _layout(rdd)
     if d is None:
-        raise ValueError("Not enough data points (0) to initialize clusters")
+        raise EmptyDataset("the dataset has no rows")
     if not np.issubdtype(np.dtype(dtype), np.floating):
         dtype = np.float64
     # balanced row blocks across partition boundaries (the takeSample layout

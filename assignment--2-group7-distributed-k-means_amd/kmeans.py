@@ -27,7 +27,7 @@ import numpy as np
 
 from . import _lib, sampling
 from .comm import Communicator
-from .dataset import DeviceBlobs, LocalRDD, Placement, place
+from .dataset import DeviceBlobs, EmptyDataset, LocalRDD, Placement, place
 from .engine import make_engine
 
 
@@ -96,18 +96,20 @@ class LloydRunner:
         size = self.batch
         while it < max_iter:
             m = min(size, max_iter - it)
-            seed = model._empty_seed()                         # int(time.time()), L196
+            # the repair seed of each iteration, int(time.time()) read per
+            # iteration as L196 reads it per repair
+            seeds = [model._empty_seed() for _ in range(m)]
             if self.device_repair == 2:
                 eng.repair_bind()
-                if eng.repair_state()[0]:                      # armed: every rank needs the same seed
-                    seed = self.comm.broadcast_obj(seed)
+                if eng.repair_state()[0]:                      # armed: every rank needs the same seeds
+                    seeds = self.comm.broadcast_obj(seeds)
             eng.batch_begin()
             try:
-                for _ in range(m):
+                for b in range(m):
                     eng.assign_stats()                         # L272 (+ L169-171 map side)
                     self.comm.allreduce_stats(eng)             # L169-173 shuffle + collect
                     # L176-206 (+ the repair's seed, L196), device convergence test
-                    eng.update_async(model.tolerance, seed)
+                    eng.update_async(model.tolerance, seeds[b])
                     if self.device_repair == 2 and eng.repair_state()[1]:
                         # the picked rows from their owners (L196-200), then the rest
                         # of the update on the device
@@ -345,7 +347,11 @@ class KMeans:
         if hasattr(rdd, "cache"):
             rdd.cache()                                        # L256
         comm = Communicator()
-        run = self._make_runner(rdd, comm)
+        try:
+            run = self._make_runner(rdd, comm)
+        except EmptyDataset:
+            # takeSample of an empty RDD returns [] (L72-74)
+            raise ValueError(f"Not enough data points (0) to initialize {self.k} clusters") from None
         self._runner, self._runner_src = run, _ref_to(rdd)
         self.centroids = self._initialize_centroids(run)       # L259
         self.sse_history = []                                  # L260
@@ -369,7 +375,10 @@ class KMeans:
         if self._runner is not None and _deref(self._runner_src) is rdd:
             run = self._runner  # the rows are resident from fit
         else:
-            run = self._make_runner(rdd, comm)
+            try:
+                run = self._make_runner(rdd, comm)
+            except EmptyDataset:
+                return LabelsRDD(np.zeros(0, dtype=np.int32), comm)  # a lazy map over no rows (L350)
         run.engine.set_centroids(np.asarray(self.centroids, dtype=np.float64))
         labels = LabelsRDD(run.engine.predict(), comm)
         if sc is not None and hasattr(sc, "_jsc") and hasattr(rdd, "getNumPartitions"):

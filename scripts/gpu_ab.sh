@@ -1,14 +1,23 @@
-# A/B of an env knob on the c3 bench (after the GPU parity tests):
-#   VAR=KM_DEFER VALS="0 1" bash scripts/gpu_ab.sh
+# A/B of library builds on one box, alternating runs (never ranks builds across
+# boxes: MI355X_MICROARCH.md 'DVFS give-back' item 5).  Each arm is a library
+# file under the package directory, selected per process through KM_LIB
+# (nothing is copied over the product library):
+#   ARMS="libkmeans_amd.so libkmeans_amd_f32.so" CFGS="c3 c5" TAG=r4_shape bash scripts/gpu_ab.sh
+# optional: ROUNDS (default 2), STEPS (default 20), WARMUP (default 3), SSE (bench --sse)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-TAG=${TAG:-ab}
-if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/${TAG}_tests.log
-  [ $rc -ne 0 ] && exit 1
-fi
-for V in ${VALS}; do
-  env $VAR=$V timeout -k 10 300 python -u bench.py --config ${CFG:-c3} --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline > gpurun_out/${TAG}_$V.json 2> gpurun_out/${TAG}_$V.err || { tail -5 gpurun_out/${TAG}_$V.err; exit 1; }
-  python -c "import json;d=json.load(open('gpurun_out/${TAG}_$V.json'));print('$VAR=$V', round(d['value'],2),'it/s', {k:round(v,3) for k,v in d['kernel_avg_ms'].items()}, d['resolve'], round(d['roofline']['frac'],3))"
+P=assignment--2-group7-distributed-k-means_amd
+OUT=gpurun_out/${TAG:-ab}; mkdir -p $OUT
+EXTRA=""
+if [ -n "${SSE:-}" ]; then EXTRA="--sse $SSE"; fi
+for CFG in ${CFGS:-c3}; do
+  for R in $(seq ${ROUNDS:-2}); do
+    for A in ${ARMS:-libkmeans_amd.so}; do
+      N=${A%.so}
+      KM_LIB=$PWD/$P/$A timeout -k 10 400 python -u bench.py --config $CFG --steps ${STEPS:-20} --warmup ${WARMUP:-3} \
+        --no-cpu-baseline $EXTRA > $OUT/$CFG.$N.$R.json 2> $OUT/$CFG.$N.$R.err || { echo "$CFG $A failed"; tail -5 $OUT/$CFG.$N.$R.err; exit 1; }
+      python3 -c "import json;d=json.load(open('$OUT/$CFG.$N.$R.json'));print('$CFG $N $R', round(d['value'],3), round(d['ms_per_step'],3), {k:round(v,3) for k,v in d['kernel_avg_ms'].items()}, d['resolve'])"
+    done
+  done
 done

@@ -117,5 +117,95 @@ class OracleEngine:
         return {"n": self.n, "d": self.d, "k": self.k, "path": 0}
 
 
+class DeviceRepairEngine(OracleEngine):
+    """The OracleEngine with the device's empty-cluster repair protocol
+    (km_set_layout / km_repair_state / km_repair_buffer /
+    km_repair_apply_async): in a batch that is "armed" the update repairs
+    empties itself by the takeSample policy (kmeans_spark.py:191-204) instead
+    of stopping the batch; with rows spread over ranks (mode 2) every rank
+    picks the same global rows, writes the ones it holds into the repair
+    buffer (zeros elsewhere), the caller all-reduces that buffer
+    (repair_exchange) and the apply step finishes the iteration.  Arming as on
+    the device: armed after new centroids, disarmed by a batch without
+    empties."""
+
+    def set_layout(self, sizes, row0, mode):
+        self.layout, self.row0, self.rep_mode = [int(v) for v in sizes], int(row0), int(mode)
+        self.armed, self.waiting, self._rep_t, self._pending = bool(mode), False, None, None
+
+    def set_centroids(self, C):
+        super().set_centroids(C)
+        self.armed = bool(getattr(self, "rep_mode", 0))
+
+    def replace_rows(self, ids, rows):
+        super().replace_rows(ids, rows)
+        self.armed = bool(self.rep_mode)
+
+    def repair_bind(self):
+        import torch
+        if self._rep_t is None or self._rep_t.numel() != self.k * self.d:
+            self._rep_t = torch.zeros(self.k * self.d, dtype=torch.float64)
+
+    def repair_state(self):
+        return bool(self.rep_mode) and self.armed, self.waiting
+
+    def update_async(self, tol, empty_seed=0):
+        if self._stopped:
+            return
+        st, counts = self.update()
+        st.repaired = 0
+        repair = bool(self.rep_mode) and self.armed
+        if repair and st.n_empty and not st.nonfinite and st.n_empty < sum(self.layout):
+            empty = [j for j in range(self.k) if counts[j] == 0]
+            gidx = orc.take_sample_indices(self.layout, len(empty), int(empty_seed))
+            buf = np.zeros(self.k * self.d)
+            for i, g in enumerate(gidx):
+                if self.row0 <= g < self.row0 + self.n:
+                    buf[i * self.d:(i + 1) * self.d] = self.X[g - self.row0]
+            self._pending = (st, counts, empty, len(gidx), tol)
+            if self.rep_mode == 2:
+                self.repair_bind()
+                self._rep_t.copy_(__import__("torch").from_numpy(buf))
+                self.waiting = True
+                return
+            self._apply(buf)
+            return
+        stop = 3 if st.nonfinite else (2 if st.n_empty else (1 if st.max_shift < tol else 0))
+        self._finish(st, counts, stop)
+
+    def repair_exchange(self, allreduce):
+        allreduce(self._rep_t)
+        self.waiting = False
+        self._apply(self._rep_t.numpy())
+
+    def _apply(self, buf):
+        st, counts, empty, num, tol = self._pending
+        rows = np.asarray(buf).reshape(self.k, self.d)[:num]
+        old = self.cur
+        for i in range(num):
+            self.new[empty[i]] = rows[i]
+        shift = np.sqrt(((self.new - old) ** 2).sum(axis=1))
+        st.max_shift = float(shift.max())
+        st.nonfinite = int(not np.all(np.isfinite(self.new)))
+        st.repaired = 1
+        self._finish(st, counts, 3 if st.nonfinite else (1 if st.max_shift < tol else 0))
+
+    def _finish(self, st, counts, stop):
+        st.stop_reason = stop
+        self._slots.append((self.cur.copy(), self.new.copy(), st, counts))
+        self._stopped = bool(stop)
+        self.cur = self.new.copy()                      # speculative commit
+
+    def batch_end(self, m):
+        out = super().batch_end(m)
+        if getattr(self, "rep_mode", 0):
+            self.armed = any(st.n_empty for st, _ in out)
+        return out
+
+
 def factory(comm):
     return OracleEngine(comm)
+
+
+def factory_device_repair(comm):
+    return DeviceRepairEngine(comm)

@@ -48,7 +48,7 @@ def test_product_library_has_no_diagnostic_kernels():
     assert fused and mfma, "kernel symbols not found"
     assert set(fused) == {"0"} and set(mfma) == {"0"}, (set(fused), set(mfma))
     # the fast-screen experiment (k_fused1, k_prep_bal) is diagnostic-only too
-    assert "k_fused1" not in syms and "k_prep_bal" not in syms
+    assert not re.search(r"k_fused1<", syms) and "k_prep_bal" not in syms
     assert "getenv" not in subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True,
                                           text=True, check=True).stdout
 
@@ -260,6 +260,38 @@ def _fit(g, inject=True):
     return km, buf.getvalue(), np.array(km.predict(rdd, sc).collect())
 
 
+def test_init_errors_match_reference(cpu_engine):
+    # kmeans_spark.py:72-80: takeSample returns [] for an empty RDD and fewer
+    # than k rows for a small one; a NaN / Inf among the sampled rows raises
+    ka = _ka()
+    sc = ka.LocalContext()
+    with pytest.raises(ValueError, match=re.escape("Not enough data points (0) to initialize 4 clusters")):
+        ka.KMeans(k=4).fit(sc.parallelize(np.zeros((0, 3)), 2), sc)
+    with pytest.raises(ValueError, match=re.escape("Not enough data points (0) to initialize 3 clusters")):
+        ka.KMeans(k=3).fit(sc.parallelize([], 1), sc)
+    with pytest.raises(ValueError, match=re.escape("Not enough data points (5) to initialize 6 clusters")):
+        ka.KMeans(k=6).fit(sc.parallelize(np.arange(10.0).reshape(5, 2), 2), sc)
+    X = np.random.default_rng(0).normal(size=(40, 3))
+    X[:, 1] = np.nan  # every row non-finite: any takeSample pick carries a NaN
+    with pytest.raises(ValueError, match=re.escape("Data contains NaN or Inf values")):
+        ka.KMeans(k=3).fit(sc.parallelize(X, 4), sc)
+    X[:, 1] = np.inf
+    with pytest.raises(ValueError, match=re.escape("Data contains NaN or Inf values")):
+        ka.KMeans(k=3).fit(sc.parallelize(X, 4), sc)
+
+
+def test_predict_on_empty_dataset_is_empty(cpu_engine):
+    # predict is a lazy map over the rows (kmeans_spark.py:343-350): no rows, no labels
+    ka = _ka()
+    sc = ka.LocalContext()
+    X = np.random.default_rng(1).normal(size=(30, 2))
+    km = ka.KMeans(k=2, max_iter=3)
+    with contextlib.redirect_stdout(io.StringIO()):
+        km.fit(sc.parallelize(X, 2), sc)
+    out = km.predict(sc.parallelize(np.zeros((0, 2)), 1), sc)
+    assert out.collect() == [] and out.count() == 0
+
+
 @pytest.mark.parametrize("name", ["test_a", "test_d", "empty", "ties", "test_c", "tight", "tight_wide", "c5_poor"])
 def test_driver_reproduces_reference_with_cpu_engine(golden, cpu_engine, name):
     from test_gpu_parity import assert_logs_match
@@ -410,7 +442,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, name, q):
+def _rank_main(rank, world, port, name, q, device_repair=False):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -423,33 +455,58 @@ def _rank_main(rank, world, port, name, q):
         import kmeans_amd as ka
         import cpu_engine as ce
         from conftest import load_golden
-        ka.KMeans._engine_factory = staticmethod(ce.factory)
+        ka.KMeans._engine_factory = staticmethod(ce.factory_device_repair if device_repair else ce.factory)
         g = load_golden(name)
         km, out, labels = _fit(g, inject=(name in INJECTED))
-        q.put((rank, km.centroids, km.sse_history, labels, out))
+        run = km._runner
+        q.put((rank, km.centroids, km.sse_history, labels, out, (run.device_repair, run.device_repairs)))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["test_a", "test_d", "empty"])
-def test_two_ranks_gloo_match_single_rank(golden, name):
+def _run_ranks(world, name, device_repair=False):
     import torch.multiprocessing as mp
-    g = golden(name)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, name, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, name, q, device_repair)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in procs], key=lambda t: t[0])
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    for rank, C, sse, labels, out in res:
+    return res
+
+
+@pytest.mark.parametrize("name", ["test_a", "test_d", "empty"])
+def test_two_ranks_gloo_match_single_rank(golden, name):
+    g = golden(name)
+    res = _run_ranks(2, name)
+    for rank, C, sse, labels, out, _ in res:
         np.testing.assert_allclose(C, g["centroids"], rtol=1e-9, atol=1e-9)
         np.testing.assert_allclose(sse, g["sse_history"], rtol=1e-9)
         np.testing.assert_array_equal(labels, g["labels"])
     assert res[0][4] and not res[1][4]  # only rank 0 logs, like the single driver
+
+
+@pytest.mark.parametrize("world,name", [(4, "c5_poor"), (4, "empty"), (1, "c5_poor")])
+def test_device_repair_protocol_over_gloo_ranks(golden, world, name):
+    # the device repair's host protocol (layout mode 2 with world > 1: the same
+    # seeds on every rank, every rank picks the same takeSample rows, the
+    # owners' rows meet in one all-reduce, the apply finishes the iteration;
+    # mode 1 on one rank) with the CPU engine standing in for the device, on
+    # the reference's own goldens (~509 empties at c5_poor's first update)
+    from test_gpu_parity import assert_logs_match
+    g = golden(name)
+    res = _run_ranks(world, name, device_repair=True)
+    for rank, C, sse, labels, out, (mode, repairs) in res:
+        assert mode == (2 if world > 1 else 1) and repairs >= 1, (mode, repairs)
+        np.testing.assert_allclose(C, g["centroids"], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(sse, g["sse_history"], rtol=1e-9)
+        np.testing.assert_array_equal(labels, g["labels"])
+    assert_logs_match(res[0][4], g["stdout"])
+    assert all(not r[4] for r in res[1:])
 
 
 class SparkLikeRDD:
@@ -627,7 +684,7 @@ def test_distributed_device_repair_enqueue_order():
 
         def broadcast_obj(self, obj, src=0):
             calls.append(("bcast", obj))
-            return 777
+            return [777 + i for i in range(len(obj))]  # one seed per iteration of the batch
 
         def allreduce_stats(self, eng):
             calls.append("allreduce_stats")
@@ -687,8 +744,8 @@ def test_distributed_device_repair_enqueue_order():
     assert run.device_repair == 2 and calls[0] == ("layout", [6, 6], 6, 2)
     run.batch = 2
     run.run(Model(), None, 4)
-    it = ["assign", "allreduce_stats", ("update", 777), "allreduce_rows", "apply"]
-    assert calls[1:] == ["bind", ("bcast", 123), "begin"] + it + it + ["commit", "bind", "begin"] + \
+    it = [["assign", "allreduce_stats", ("update", 777 + i), "allreduce_rows", "apply"] for i in range(2)]
+    assert calls[1:] == ["bind", ("bcast", [123, 123]), "begin"] + it[0] + it[1] + ["commit", "bind", "begin"] + \
         ["assign", "allreduce_stats", ("update", 123)] * 2 + ["commit"], calls
 
 
