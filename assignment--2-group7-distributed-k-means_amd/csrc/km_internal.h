@@ -64,13 +64,32 @@ hipError_t launch_prep_small(const double* C64, const Geometry& g, float* C32, f
 hipError_t launch_prep_split(const float* C32, const Geometry& g, const float* cn2, const float* xabs,
                              const float* cabs, _Float16* Chi, _Float16* Clo, float* cn2s, const int* gate, hipStream_t s);
 hipError_t launch_absmax(const float* X, int64_t nfloats, float* out, hipStream_t s);
-// Small k*d path: direct-form fp32 screening, in-thread exact re-rank,
+// Small k*d path: direct-form fp32 screening (ambiguous rows queued, see below),
 // optional fused statistics (LDS float64 table, replicated per lane).
 // want_sse: also add every point's float64 residual ||x - c_label||^2 to
 // stats[k (d+1)] (the SSE slot, kmeans_spark.py:224-237)
+// The rows the fp32 bound cannot settle are queued; the last workgroup of the
+// launch resolves them in float64 (and adds their sums) and, with fold, runs
+// the one-workgroup update as well (an iteration in one launch).
+struct SmallTail {
+  uint32_t* queue;  // ambiguous rows (capacity n)
+  uint32_t* qctr;   // queue length; zeroed again by the last workgroup
+  uint32_t* done;   // [0] workgroups finished, [1] queued rows; zeroed again by the last workgroup
+  int fold;         // run the one-workgroup update in the last workgroup
+  const double* old;
+  double* out;
+  int64_t* counts;
+  DevStatus* st;
+  int* gate;
+  double stop_tol;
+  int dev_repair;
+  float* C32n;  // the next iteration's images (prep folded in), or nullptr
+  float* cmaxn;
+  int kp;
+};
 hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C32, const double* C64,
                                const float* cmax, int32_t* labels, double* stats, int fuse_stats, int want_sse,
-                               int n_cu, const int* gate, hipStream_t s);
+                               int n_cu, const int* gate, hipStream_t s, const SmallTail& tail);
 bool small_path_ok(const Geometry& g);
 // MFMA path: fp16x3 screening on v_mfma_f32_32x32x16_f16, top-3 keys,
 // ambiguous points queued for the exact resolvers.

@@ -258,21 +258,49 @@ hipError_t launch_prep_centroids(const double* C64, const Geometry& g, float* C3
 // per lane (no same-address atomics inside a 32-lane group).
 // ---------------------------------------------------------------------------
 static constexpr int SMALL_MAX_K = 32;
+static constexpr int SMALL_QW = 32;  // queued rows a wave resolves itself (LDS); more go to the last workgroup
 static constexpr int SMALL_LDS = 60 * 1024;
 
-// KU > 0: k <= KU, loops over centroids unrolled and the fp32 centroids held
-// in registers (no LDS reads queued behind the statistics atomics)
-template <int DP, int KU = 0>
-__global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k,
-                                                      const float* __restrict__ C32,
-                                                      const double* __restrict__ C64,
-                                                      const float* __restrict__ cmaxp, int32_t* __restrict__ labels,
-                                                      double* __restrict__ stats, int fuse, int want_sse, int R, const int* __restrict__ gate) {
-  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
+// The rows the direct-form bound cannot settle (rare: q_rerank 0 at c2 in
+// steady state) are queued instead of re-ranked in-thread: the float64
+// re-rank's registers held the kernel at 4 waves per SIMD (125 VGPRs) while
+// it never ran.  The last workgroup to finish (done counter) resolves the
+// queue -- the reference's float64 norms in NumPy's order, np.argmin's
+// tie-break -- adds those rows' sums, counts and residuals, and, when the
+// iteration is local (one rank: no all-reduce between the sums and the
+// update), runs the one-workgroup update itself, so an iteration is one
+// launch (update_one_body; launch_assign_small's SmallTail).
+
+template <bool COHERENT>
+__device__ void update_one_body(double* __restrict__ stats, const double* __restrict__ old, int k, int d,
+                                double* __restrict__ out, int64_t* __restrict__ counts, const double* __restrict__ sse,
+                                const uint32_t* __restrict__ qcount, uint32_t nq, DevStatus* __restrict__ st,
+                                int* __restrict__ gate, double stop_tol, int dev_repair, int clear,
+                                float* __restrict__ C32, float* __restrict__ cmax, int dp, int kp);
+
+// 8 waves per SIMD at dp = 16 (c2: 32 VGPRs of row and prefetch), the
+// compiler's choice above (a row and its prefetch are 2 dp VGPRs)
+#ifndef KM_SMALL_WPE
+#define KM_SMALL_WPE 8
+#endif
+template <int DP, bool SSE, int WPE = (DP <= 16 ? KM_SMALL_WPE : 1)>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const float* __restrict__ C32,
+                    const double* __restrict__ C64, const float* __restrict__ cmaxp, int32_t* __restrict__ labels,
+                    double* __restrict__ stats, int fuse, int R, const int* __restrict__ gate, SmallTail T) {
+  constexpr bool want_sse = SSE;
+  if (*gate) {  // a stopped batch (km_update_async): the rest of it is a no-op
+    if (T.fold && blockIdx.x == 0 && threadIdx.x == 0) {
+      T.st->ran = 0;
+      T.st->stop = 0;
+    }
+    return;
+  }
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* sC = reinterpret_cast<float*>(smem);
   double* tab = reinterpret_cast<double*>(smem + ((k * DP * 4 + 15) / 16) * 16);
   const int d1 = d + 1;
+  const int lane = threadIdx.x & 63;
   for (int i = threadIdx.x; i < k * DP; i += blockDim.x) sC[i] = C32[i];
   if (fuse)
     for (int i = threadIdx.x; i < k * d1 * R; i += blockDim.x) tab[i] = 0.0;
@@ -286,21 +314,22 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
   const float beta = 2.0f * 2.5f * U24 * cm;
   const float g0 = 2.0f * 8.0f * U24 * U24 * cm * cm;
   const int rep = threadIdx.x & (R - 1);
-  float cr[KU > 0 ? KU : 1][DP];
-  if constexpr (KU > 0) {
-#pragma unroll
-    for (int j = 0; j < KU; ++j)
-#pragma unroll
-      for (int f = 0; f < DP; ++f) cr[j][f] = j < k ? sC[j * DP + f] : 0.0f;
-  }
 
   // rows strided over the grid; the next row is prefetched into registers
   // while this one is processed (the loop is otherwise latency-bound)
   const int64_t rstride = (int64_t)gridDim.x * blockDim.x;
   int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double sacc = 0.0;  // this lane's SSE residuals (want_sse)
+  // this wave's queued rows (LDS, after the statistics table)
+  uint32_t* wq = reinterpret_cast<uint32_t*>(smem + ((k * DP * 4 + 15) / 16) * 16 + (fuse ? (size_t)k * d1 * R * 8 : 0)) +
+                 (threadIdx.x >> 6) * SMALL_QW;
+  uint32_t wq_n = 0;
+  // PF: the next row prefetched into registers while this one is processed
+  // (at 8 waves per SIMD the other waves hide the latency instead: no
+  // prefetch, 2 dp fewer VGPRs)
+  constexpr bool PF = WPE < 8;
   float4 nx[DP / 4];
-  if (row < n) {
+  if (PF && row < n) {
 #pragma unroll
     for (int f = 0; f < DP; f += 4) nx[f / 4] = *reinterpret_cast<const float4*>(X + row * DP + f);
   }
@@ -308,33 +337,23 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
     float x[DP];
 #pragma unroll
     for (int f = 0; f < DP; f += 4) {
-      const float4 v = nx[f / 4];
+      const float4 v = PF ? nx[f / 4] : *reinterpret_cast<const float4*>(X + row * DP + f);
       x[f] = v.x;
       x[f + 1] = v.y;
       x[f + 2] = v.z;
       x[f + 3] = v.w;
     }
-    if (row + rstride < n) {
+    if (PF && row + rstride < n) {
 #pragma unroll
       for (int f = 0; f < DP; f += 4) nx[f / 4] = *reinterpret_cast<const float4*>(X + (row + rstride) * DP + f);
     }
     float k1 = FLT_MAX, k2 = FLT_MAX, k3 = FLT_MAX;
-    if constexpr (KU > 0) {
-#pragma unroll
-      for (int j = 0; j < KU; ++j) {
-        float acc = 0.0f;
-#pragma unroll
-        for (int f = 0; f < DP; ++f) {
-          const float t = x[f] - cr[j][f];
-          acc = fmaf(t, t, acc);
-        }
-        if (j < k) top3_insert(k1, k2, k3, key_of(acc, (uint32_t)j, mask));
-      }
-    } else {
+    {
       // packed fp32 (v_pk_add_f32 / v_pk_fma_f32): even and odd features in
       // two partial sums, half the VALU issue of the scalar loop; the
       // direct-form bound (DP sequential terms) covers two sums of DP / 2
       typedef float f32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll 2
       for (int j = 0; j < k; ++j) {
         const f32x2* c2 = reinterpret_cast<const f32x2*>(sC + j * DP);
         f32x2 acc2 = {0.0f, 0.0f};
@@ -348,29 +367,28 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
       }
     }
     int lab = (int)(__float_as_uint(k1) & mask);
-    const int i2 = (int)(__float_as_uint(k2) & mask);
     const float B1 = alpha * k1 + beta * sqrtf(k1) + g0;
     const float B2 = alpha * k2 + beta * sqrtf(k2) + g0;
-    const float B3 = alpha * k3 + beta * sqrtf(k3) + g0;
-    const bool need_full = (k >= 3) && !((k3 > 64.0f * U24 * U24 * cm * cm) && (k3 - B3 > k1 + B1));
-    const bool need_two = (k >= 2) && !(k2 - B2 > k1 + B1);
-    if (need_full || need_two) {
-      // the reference's float64 norms with the point held in registers
-      double best = 0.0;
-      int bl = -1;
-      const int jn = need_full ? k : 2;
-      for (int jj = 0; jj < jn; ++jj) {
-        const int j = need_full ? jj : (jj == 0 ? (lab < i2 ? lab : i2) : (lab < i2 ? i2 : lab));
-        const double v = np_norm_reg<DP>(x, C64 + (size_t)j * d, d);
-        if (np_better(v, best, bl >= 0)) {
-          best = v;
-          bl = j;
+    const bool amb = (k >= 2) && !(k2 - B2 > k1 + B1);  // k1 not provably the float64 argmin
+    if (lab >= k) lab = 0;  // only reachable with non-finite data (np.argmin of NaNs -> 0)
+    // a queued row's label is written by the last workgroup only (two
+    // writers of one label in one launch could reach memory in either order)
+    if (!amb) labels[row] = lab;
+    const uint64_t qm = __ballot(amb);
+    if (qm) {  // rare: the wave's own LDS queue, past SMALL_QW rows the launch's queue
+      const uint32_t pos = wq_n + (uint32_t)__popcll(qm & ((1ull << lane) - 1ull));
+      if (amb) {
+        if (pos < SMALL_QW) {
+          wq[pos] = (uint32_t)row;
+        } else {
+          // write-through (sc1) store: the last workgroup may sit on another XCD
+          const uint32_t g = atomicAdd(T.qctr, 1u);
+          __hip_atomic_store(T.queue + g, (uint32_t)row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
-      lab = bl;
+      wq_n += (uint32_t)__popcll(qm);
     }
-    if (lab >= k) lab = 0;  // only reachable with non-finite data (np.argmin of NaNs -> 0)
-    labels[row] = lab;
+    if (amb) continue;
     if (want_sse) {
       // min(norm)**2 of compute_partition_sse (kmeans_spark.py:231-233): the
       // residual to the pre-update centroid, each difference and square in
@@ -393,9 +411,76 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
       atomicAdd(t + (size_t)d * R, 1.0);
     }
   }
+  // A queued row, resolved by one wave, lanes over centroids: the
+  // reference's float64 norms (kmeans_spark.py:153) in NumPy's pairwise
+  // order, np.argmin's tie-break across the lanes; the row's sums go to the
+  // LDS table (in_lds) or straight to the global statistics; returns its
+  // residual (want_sse) in every lane
+  auto resolve = [&](int64_t r, bool in_lds) {
+    const float* xr = X + r * DP;
+    double v = 0.0;
+    int j = -1;
+    if (lane < k) {
+      v = np_norm_d<0>([&](int f) { return np_sq(C64[(size_t)lane * d + f], xr[f]); }, d);  // d <= 64: one block
+      j = lane;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {  // first NaN, else the smallest, lowest index
+      const double ov = __shfl_xor(v, o);
+      const int oj = __shfl_xor(j, o);
+      bool take = false;
+      if (oj >= 0) {
+        if (j < 0) {
+          take = true;
+        } else {
+          const bool on = ov != ov, mn = v != v;
+          take = (on && !mn) || (on == mn && (on ? oj < j : (ov < v || (ov == v && oj < j))));
+        }
+      }
+      if (take) {
+        v = ov;
+        j = oj;
+      }
+    }
+    const int lab = j < 0 ? 0 : j;
+    if (lane == 0) {
+      if (in_lds)
+        labels[r] = lab;
+      else  // write-through: no other writer of this label in the launch, but keep it out of this XCD's L2
+        __hip_atomic_store(labels + r, lab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    double rr = 0.0;
+    for (int f = lane; f < d; f += 64) {
+      const double x = (double)xr[f];
+      if (fuse) {
+        if (in_lds)
+          atomicAdd(tab + ((size_t)lab * d1 + f) * R, x);
+        else
+          atomicAdd(stats + (size_t)lab * d1 + f, x);
+      }
+      const double t = x - C64[(size_t)lab * d + f];
+      rr = fma(t, t, rr);
+    }
+    if (fuse && lane == 0) {
+      if (in_lds)
+        atomicAdd(tab + ((size_t)lab * d1 + d) * R, 1.0);
+      else
+        atomicAdd(stats + (size_t)lab * d1 + d, 1.0);
+    }
+    return want_sse ? wave_sum(rr) : 0.0;
+  };
+  {
+    const uint32_t nall = (uint32_t)__builtin_amdgcn_readfirstlane(wq_n);
+    if (nall && lane == 0) atomicAdd(T.done + 1, nall);  // queued rows of the launch (status q_rerank)
+    const uint32_t nw = min(nall, (uint32_t)SMALL_QW);
+    for (uint32_t i = 0; i < nw; ++i) {
+      const double rs = resolve(wq[i], true);
+      if (lane == 0) sacc += rs;
+    }
+  }
   if (want_sse) {
     sacc = wave_sum(sacc);
-    if ((threadIdx.x & 63) == 0 && sacc != 0.0) atomicAdd(stats + (size_t)k * d1, sacc);
+    if (lane == 0 && sacc != 0.0) atomicAdd(stats + (size_t)k * d1, sacc);
   }
   if (fuse) {
     __syncthreads();
@@ -404,6 +489,41 @@ __global__ __launch_bounds__(256) void k_assign_small(const float* __restrict__ 
       for (int r = 0; r < R; ++r) s += tab[(size_t)e * R + r];
       if (s != 0.0) atomicAdd(stats + e, s);
     }
+  }
+  // ---- the last workgroup: queued rows, then (fold) the update ----
+  // Hand-off without an L2 write-back (cdna_hip_programming.md section 6,
+  // the counter form with write-through data): everything the last
+  // workgroup reads was written by device-scope atomics (sums, counter) or
+  // sc1 stores (queue); each wave drains them (vmcnt), then one relaxed
+  // agent-scope ticket per workgroup; the last reads with sc1 loads.
+  // (__threadfence() here -- a full XCD L2 write-back per workgroup -- made
+  // the c2 launch 3.5x slower.)
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(T.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
+  __syncthreads();
+  if (!s_last) return;
+  const uint32_t nq = __hip_atomic_load(T.qctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the rows past the waves' own queues: one per wave
+  const int wave = threadIdx.x >> 6;
+  double qs = 0.0;
+  for (uint32_t i = wave; i < nq; i += blockDim.x >> 6)
+    qs += resolve(__hip_atomic_load(T.queue + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), false);
+  if (want_sse && lane == 0 && qs != 0.0) atomicAdd(stats + (size_t)k * d1, qs);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the queued rows' sums are in before the update reads them
+  __syncthreads();
+  if (T.fold) {
+    update_one_body<true>(stats, T.old, k, d, T.out, T.counts, stats + (size_t)k * d1, nullptr, 0u, T.st, T.gate,
+                          T.stop_tol, T.dev_repair, 1, T.C32n, T.cmaxn, DP, T.kp);
+    if (threadIdx.x == 0)
+      T.st->q_rerank = (int32_t)__hip_atomic_load(T.done + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) {
+    T.done[0] = 0u;
+    T.done[1] = 0u;
+    *T.qctr = 0u;
   }
 }
 
@@ -419,11 +539,15 @@ int diag_env(const char* name, int dflt) {
 #endif
 }
 
+// statistics replicas: as many as fit the LDS share of one of the 8
+// workgroups a CU holds at 8 waves per SIMD (20 KiB each), at most 32
+static constexpr int SMALL_WG_LDS = 20 * 1024;
 static int small_replicas(const Geometry& g) {
   const size_t cbytes = ((size_t)g.k * g.dp * 4 + 15) / 16 * 16;
   static const int rmax = diag_env("KM_SMALL_R", 32);
+  static const int budget = diag_env("KM_SMALL_LDS", SMALL_WG_LDS);
   int R = rmax;
-  while (R > 1 && cbytes + (size_t)g.k * (g.d + 1) * 8 * R > SMALL_LDS) R >>= 1;
+  while (R > 1 && cbytes + (size_t)g.k * (g.d + 1) * 8 * R > (size_t)budget) R >>= 1;
   return R;
 }
 
@@ -435,34 +559,31 @@ bool small_path_ok(const Geometry& g) {
 
 hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C32, const double* C64,
                                const float* cmax, int32_t* labels, double* stats, int fuse, int want_sse, int n_cu,
-                               const int* gate, hipStream_t s) {
+                               const int* gate, hipStream_t s, const SmallTail& tail) {
   if (g.n == 0) return hipSuccess;
+  if (!tail.queue || !tail.qctr || !tail.done) return hipErrorInvalidValue;
   const int R = small_replicas(g);
-  const size_t lds = ((size_t)g.k * g.dp * 4 + 15) / 16 * 16 + (fuse ? (size_t)g.k * (g.d + 1) * 8 * R : 0);
+  const size_t lds = ((size_t)g.k * g.dp * 4 + 15) / 16 * 16 + (fuse ? (size_t)g.k * (g.d + 1) * 8 * R : 0) +
+                     (size_t)4 * SMALL_QW * 4;
   int64_t blocks = (g.n + 255) / 256;
-  static const int bpc = diag_env("KM_SMALL_BPC", 4);
+  static const int bpc = diag_env("KM_SMALL_BPC", 8);
   const int64_t cap = (int64_t)n_cu * bpc;
   if (blocks > cap) blocks = cap;
+#define KM_SMALL_CASE(DP_)                                                                                 \
+  case DP_:                                                                                                \
+    if (want_sse)                                                                                          \
+      hipLaunchKernelGGL((k_assign_small<DP_, true>), dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d, \
+                         g.k, C32, C64, cmax, labels, stats, fuse, R, gate, tail);                         \
+    else                                                                                                   \
+      hipLaunchKernelGGL((k_assign_small<DP_, false>), dim3((unsigned)blocks), dim3(256), lds, s, X, g.n,     \
+                         g.d, g.k, C32, C64, cmax, labels, stats, fuse, R, gate, tail);                    \
+    break;
   switch (g.dp) {
-    case 16:
-      hipLaunchKernelGGL(k_assign_small<16>, dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d, g.k, C32, C64,
-                         cmax, labels, stats, fuse, want_sse, R, gate);
-      break;
-    case 32:
-      hipLaunchKernelGGL(k_assign_small<32>, dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d, g.k, C32, C64,
-                         cmax, labels, stats, fuse, want_sse, R, gate);
-      break;
-    case 48:
-      hipLaunchKernelGGL(k_assign_small<48>, dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d, g.k, C32, C64,
-                         cmax, labels, stats, fuse, want_sse, R, gate);
-      break;
-    case 64:
-      hipLaunchKernelGGL(k_assign_small<64>, dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d, g.k, C32, C64,
-                         cmax, labels, stats, fuse, want_sse, R, gate);
-      break;
+    KM_SMALL_CASE(16) KM_SMALL_CASE(32) KM_SMALL_CASE(48) KM_SMALL_CASE(64)
     default:
       return hipErrorInvalidValue;
   }
+#undef KM_SMALL_CASE
   return hipGetLastError();
 }
 
@@ -484,6 +605,34 @@ static constexpr int MFMA_LDS_LARGE = 160 * 1024;  // LDS per CU
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+// lo = RN_f16(xs - hi) for a pair, hi = RN_f16(xs) (the fp16x3 row split).
+// Written in C: the compiler turns it into v_fma_mix forms with the scale
+// folded in and pads the VALU -> MFMA operand hazard itself.  The
+// inline-asm form (KM_SPLIT_ASM=1, one v_fma_mix per element, rounds 1-3)
+// is not safe: hipcc placed an asm v_fma_mixhi_f16 one wait state before the
+// MFMA that reads its register as the B operand -- compiler-emitted VALU
+// writes get two -- and k_fused16 then read stale row halves (567 of 20,000
+// labels wrong in the far-from-origin test, 0 with this form; DESIGN.md
+// section 4).  k_fused's asm happened to be scheduled two or more apart.
+#ifndef KM_SPLIT_ASM
+#define KM_SPLIT_ASM 0
+#endif
+__device__ __forceinline__ f16x2 split_lo(f16x2 hp, float xs0, float xs1) {
+#if !KM_SPLIT_ASM
+  // xs - hi is exact in fp32; the compiler emits its own v_fma_mix form
+  // (with the scale folded in) and sees the writes it must pad
+  const f16x2 lo = {(_Float16)(xs0 - (float)hp[0]), (_Float16)(xs1 - (float)hp[1])};
+  return lo;
+#else
+  uint32_t lp;
+  asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lp) : "v"(__builtin_bit_cast(uint32_t, hp)), "v"(xs0));
+  asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "+v"(lp)
+      : "v"(__builtin_bit_cast(uint32_t, hp)), "v"(xs1));
+  return __builtin_bit_cast(f16x2, lp);
+#endif
+}
+
 
 // power-of-two scale: max(|x|, |c|) * s < 2^14 (so |-2cs| < 2^15 < 65504);
 // 1 for non-finite or all-zero data (the keys then force the exact path)
@@ -1556,12 +1705,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       for (int e = 0; e < 8; e += 2) {
         const float xs0 = xv[e] * s, xs1 = xv[e + 1] * s;
         const f16x2 hp = {(_Float16)xs0, (_Float16)xs1};
-        uint32_t lp;
-        asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
-            "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-            : "=&v"(lp)
-            : "v"(__builtin_bit_cast(uint32_t, hp)), "v"(xs0), "v"(xs1));
-        const f16x2 lo = __builtin_bit_cast(f16x2, lp);
+        const f16x2 lo = split_lo(hp, xs0, xs1);
         bh[t][e] = hp[0];
         bh[t][e + 1] = hp[1];
         bl[t][e] = lo[0];
@@ -2003,17 +2147,7 @@ __global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
         for (int e = 0; e < 8; e += 2) {
           const float xs0 = xv[e] * s, xs1 = xv[e + 1] * s;
           const f16x2 hp = {(_Float16)xs0, (_Float16)xs1};
-#if KM_SPLIT_ASM
-          uint32_t lp;
-          asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
-              "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-              : "=&v"(lp)
-              : "v"(__builtin_bit_cast(uint32_t, hp)), "v"(xs0), "v"(xs1));
-          const f16x2 lo = __builtin_bit_cast(f16x2, lp);
-#else
-          // xs - hi is exact in fp32: the same bits as the fused mix form
-          const f16x2 lo = {(_Float16)(xs0 - (float)hp[0]), (_Float16)(xs1 - (float)hp[1])};
-#endif
+          const f16x2 lo = split_lo(hp, xs0, xs1);
           bh[pg][t][e] = hp[0];
           bh[pg][t][e + 1] = hp[1];
           bl[pg][t][e] = lo[0];
@@ -2411,12 +2545,7 @@ __global__ __launch_bounds__(256, 1) void k_fusedp(FusedArgs A) {
     for (int e = 0; e < 8; e += 2) {
       const float xs0 = xv[e] * s, xs1 = xv[e + 1] * s;
       const f16x2 hp = {(_Float16)xs0, (_Float16)xs1};
-      uint32_t lp;
-      asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
-          "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-          : "=&v"(lp)
-          : "v"(__builtin_bit_cast(uint32_t, hp)), "v"(xs0), "v"(xs1));
-      const f16x2 lo = __builtin_bit_cast(f16x2, lp);
+      const f16x2 lo = split_lo(hp, xs0, xs1);
       bh[e] = hp[0];
       bh[e + 1] = hp[1];
       bl[e] = lo[0];
@@ -2563,12 +2692,7 @@ __global__ __launch_bounds__(256, 1) void k_fusedp(FusedArgs A) {
       asm("" : "+v"(x1));
       const float xs0 = x0 * s, xs1 = x1 * s;
       const f16x2 hp = {(_Float16)xs0, (_Float16)xs1};
-      uint32_t lp;
-      asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
-          "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-          : "=&v"(lp)
-          : "v"(__builtin_bit_cast(uint32_t, hp)), "v"(xs0), "v"(xs1));
-      const f16x2 lo = __builtin_bit_cast(f16x2, lp);
+      const f16x2 lo = split_lo(hp, xs0, xs1);
       bhn[t][e] = hp[0];
       bhn[t][e + 1] = hp[1];
       bln[t][e] = lo[0];
@@ -3013,12 +3137,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_fused1(FusedArgs A, const flo
         bh[t][e] = hp[0];
         bh[t][e + 1] = hp[1];
         if constexpr (NX == 2) {
-          uint32_t lp;
-          asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
-              "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-              : "=&v"(lp)
-              : "v"(__builtin_bit_cast(uint32_t, hp)), "v"(xs0), "v"(xs1));
-          const f16x2 lo = __builtin_bit_cast(f16x2, lp);
+          const f16x2 lo = split_lo(hp, xs0, xs1);
           bl[t][e] = lo[0];
           bl[t][e + 1] = lo[1];
         }
@@ -3352,7 +3471,7 @@ bool fast_path_ok(const Geometry& g) { return g.dp == 64 && g.kp == 256; }
 // k_fused16 (v_mfma_f32_16x16x32_f16) for dp a multiple of 32; KM_FUSED16=0
 // builds the 32x32x16 k_fused everywhere (A/B arm, make alt)
 #ifndef KM_FUSED16
-#define KM_FUSED16 0
+#define KM_FUSED16 1
 #endif
 bool fused16_ok(const Geometry& g) {
   static const int on = diag_env("KM_FUSED16", KM_FUSED16);
@@ -4616,20 +4735,22 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ wor
 // with C32 it writes the small path's images of the new centroids -- the
 // fp32 copy and max ||c||, exactly as k_prep_small (same per-lane fma order
 // over f < dp, same wave sums) -- so the next assign needs no prep launch.
-__global__ __launch_bounds__(1024) void k_update_one(double* __restrict__ stats, const double* __restrict__ old,
-                                                     int k, int d, double* __restrict__ out,
-                                                     int64_t* __restrict__ counts, const double* __restrict__ sse,
-                                                     const uint32_t* __restrict__ qcount, uint32_t nq,
-                                                     DevStatus* __restrict__ st, int* __restrict__ gate,
-                                                     double stop_tol, int dev_repair, int clear, float* __restrict__ C32,
-                                                     float* __restrict__ cmax, int dp, int kp) {
-  if (*gate) {
-    if (threadIdx.x == 0) {
-      st->ran = 0;
-      st->stop = 0;
-    }
-    return;
-  }
+// the one-workgroup update (blockDim.x <= 1024): k_update_one, and the last
+// workgroup of k_assign_small when the update is folded into the assign
+// launch (COHERENT: the statistics were summed by other workgroups of the same
+// launch; read at device scope)
+template <bool COHERENT>
+__device__ void update_one_body(double* __restrict__ stats, const double* __restrict__ old, int k, int d,
+                                double* __restrict__ out, int64_t* __restrict__ counts, const double* __restrict__ sse,
+                                const uint32_t* __restrict__ qcount, uint32_t nq, DevStatus* __restrict__ st,
+                                int* __restrict__ gate, double stop_tol, int dev_repair, int clear,
+                                float* __restrict__ C32, float* __restrict__ cmax, int dp, int kp) {
+  auto ld = [](const double* p) {
+    if constexpr (COHERENT)
+      return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      return *p;
+  };
   __shared__ double s_max[16];
   __shared__ int s_emp[16], s_nf[16], s_q[16], s_qf[16];
   __shared__ unsigned int s_cm[16];
@@ -4639,11 +4760,11 @@ __global__ __launch_bounds__(1024) void k_update_one(double* __restrict__ stats,
   int emp = 0, nf = 0, qa = 0, qb = 0;
   unsigned int cmb = 0u;  // max ||c|| bits (k_prep_small)
   for (int j = wave; j < k; j += nw) {
-    const double cnt = stats[(size_t)j * d1 + d];
+    const double cnt = ld(stats + (size_t)j * d1 + d);
     double sh = 0.0, nfl = 0.0, nn = 0.0;
     for (int f = lane; f < (C32 ? dp : d); f += 64) {
       if (f < d) {
-        const double S = stats[(size_t)j * d1 + f];
+        const double S = ld(stats + (size_t)j * d1 + f);
         const double o = old[(size_t)j * d + f];
         const double nv = (cnt > 0.0) ? S / cnt : o;
         out[(size_t)j * d + f] = nv;
@@ -4689,7 +4810,7 @@ __global__ __launch_bounds__(1024) void k_update_one(double* __restrict__ stats,
     s_cm[wave] = cmb;
   }
   __syncthreads();
-  const double sse_v = *sse;
+  const double sse_v = ld(sse);
   __syncthreads();  // every read of the statistics is done
   if (clear)
     for (int i = threadIdx.x; i < k * d1 + 1; i += blockDim.x) stats[i] = 0.0;
@@ -4724,6 +4845,24 @@ __global__ __launch_bounds__(1024) void k_update_one(double* __restrict__ stats,
     st->stop = stop;
     if (stop) *gate = stop;
   }
+}
+
+__global__ __launch_bounds__(1024) void k_update_one(double* __restrict__ stats, const double* __restrict__ old,
+                                                     int k, int d, double* __restrict__ out,
+                                                     int64_t* __restrict__ counts, const double* __restrict__ sse,
+                                                     const uint32_t* __restrict__ qcount, uint32_t nq,
+                                                     DevStatus* __restrict__ st, int* __restrict__ gate,
+                                                     double stop_tol, int dev_repair, int clear, float* __restrict__ C32,
+                                                     float* __restrict__ cmax, int dp, int kp) {
+  if (*gate) {
+    if (threadIdx.x == 0) {
+      st->ran = 0;
+      st->stop = 0;
+    }
+    return;
+  }
+  update_one_body<false>(stats, old, k, d, out, counts, sse, qcount, nq, st, gate, stop_tol, dev_repair, clear, C32,
+                         cmax, dp, kp);
 }
 
 bool update_one_ok(const Geometry& g) { return g.k <= 64 && (size_t)g.k * g.d <= 16384; }

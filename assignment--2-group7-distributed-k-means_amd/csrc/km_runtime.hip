@@ -98,6 +98,11 @@ struct km_ctx {
   int32_t* labels = nullptr;
   km::QEntry* queue = nullptr;
   uint32_t* qcount = nullptr;
+  uint32_t* small_ctr = nullptr;  // small path: queue length, finished workgroups, queued rows (k_assign_small)
+  // small path, one rank: km_assign_stats defers its launch and km_update_async
+  // launches assign + update as one kernel (the last workgroup updates)
+  bool assign_pending = false;
+  bool stats_exported = false;  // km_stats_buffer handed the buffer out: a caller may reduce it in between
   uint32_t* cand = nullptr;      // candidate-list pool of the MFMA screen (kind-4 entries)
   uint32_t* cand_ctr = nullptr;  // its per-launch record counter
   uint32_t cand_cap = 0;         // records
@@ -258,6 +263,8 @@ void free_data(km_ctx* c) {
   dfree(c->labels);
   dfree(c->queue);
   dfree(c->qcount);
+  dfree(c->small_ctr);
+  c->assign_pending = false;
   dfree(c->cand);
   dfree(c->cand_ctr);
   c->cand_cap = 0;
@@ -346,6 +353,35 @@ int ensure_repair(km_ctx* c) {
   return KM_OK;
 }
 
+// the small path's queue (the QEntry queue's storage as row indices: its
+// capacity holds n of them) and counters; no update folded in
+km::SmallTail small_tail(km_ctx* c) {
+  km::SmallTail t{};
+  t.queue = reinterpret_cast<uint32_t*>(c->queue);
+  t.qctr = c->small_ctr;
+  t.done = c->small_ctr + 1;
+  t.kp = c->g.kp;
+  return t;
+}
+
+// the update folds into the assign launch: small path, one workgroup update,
+// the context's own statistics (no caller reduces them between assign and
+// update), no device repair behind it
+bool fold_ok(km_ctx* c) {
+  return c->in_batch && c->path == 1 && km::update_one_ok(c->g) && c->stats == c->stats_own && !c->stats_exported &&
+         !(c->rep_enabled && c->rep_armed);
+}
+
+int run_assign(km_ctx* c, bool with_stats);
+
+// a deferred km_assign_stats launched on its own (any call but km_update_async
+// that follows it)
+int flush_assign(km_ctx* c) {
+  if (!c->assign_pending) return KM_OK;
+  c->assign_pending = false;
+  return run_assign(c, true);
+}
+
 int run_assign(km_ctx* c, bool with_stats) {
   const km::Geometry& g = c->g;
   if (c->prep_of != c->C64_cur) {
@@ -360,7 +396,7 @@ int run_assign(km_ctx* c, bool with_stats) {
   if (c->path == 1) {
     ProfScope ps(c, KM_K_ASSIGN);
     KM_HIP(km::launch_assign_small(c->X, g, c->C32, c->C64_cur, c->cmax, c->labels, c->stats, with_stats ? 1 : 0,
-                                   sse ? 1 : 0, c->n_cu, c->gate, c->stream));
+                                   sse ? 1 : 0, c->n_cu, c->gate, c->stream, small_tail(c)));
     return KM_OK;
   }
   if (c->fused) {
@@ -505,6 +541,10 @@ int km_set_stream(km_ctx* c, void* s) {
 int km_sync(km_ctx* c) {
   KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
   KM_HIP(hipSetDevice(c->device));
+  {
+    const int rcf = flush_assign(c);
+    if (rcf != KM_OK) return rcf;
+  }
   KM_HIP(hipStreamSynchronize(c->stream));
 #ifdef KM_DIAG
   if (km::diag_env("KM_ABLATE", 0) == 7 || km::diag_env("KM_ABLATE", 0) == 9) km::dump_fused_stamps();
@@ -544,6 +584,8 @@ int km_load_begin(km_ctx* c, int64_t n, int32_t d) {
   KM_HIP(hipMalloc(&c->labels, sizeof(int32_t) * rows));
   KM_HIP(hipMalloc(&c->queue, sizeof(km::QEntry) * km::queue_capacity(rows, c->n_cu)));
   KM_HIP(hipMalloc(&c->qcount, sizeof(uint32_t) * km::qcount_words(c->n_cu)));
+  KM_HIP(hipMalloc(&c->small_ctr, sizeof(uint32_t) * 3));
+  KM_HIP(hipMemsetAsync(c->small_ctr, 0, sizeof(uint32_t) * 3, c->stream));
   KM_HIP(hipMalloc(&c->moments, sizeof(double) * (d + 1)));
   KM_HIP(hipMalloc(&c->xabs, sizeof(float)));
   KM_HIP(hipMalloc(&c->xnorm, sizeof(float) * rows));
@@ -646,6 +688,10 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
   KM_REQUIRE(d == c->g.d, KM_ERR_ARG,
              "km_set_centroids: d=" + std::to_string(d) + " != data d=" + std::to_string(c->g.d));
   KM_HIP(hipSetDevice(c->device));
+  {
+    const int rcf = flush_assign(c);
+    if (rcf != KM_OK) return rcf;
+  }
   if (k != c->k_alloc) {
     KM_HIP(hipStreamSynchronize(c->stream));
     double* external = (c->stats && c->stats != c->stats_own) ? c->stats : nullptr;
@@ -704,6 +750,10 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
 int km_get_centroids(km_ctx* c, int32_t which, double* out) {
   KM_REQUIRE(c && c->have_c && out, KM_ERR_STATE, "km_get_centroids: no centroids");
   KM_HIP(hipSetDevice(c->device));
+  {
+    const int rcf = flush_assign(c);
+    if (rcf != KM_OK) return rcf;
+  }
   const double* src = which ? c->C64_new : c->C64_cur;
   KM_HIP(hipMemcpyAsync(out, src, sizeof(double) * c->g.k * c->g.d, hipMemcpyDeviceToHost, c->stream));
   KM_HIP(hipStreamSynchronize(c->stream));
@@ -715,11 +765,27 @@ int km_assign_stats(km_ctx* c) {
   KM_REQUIRE(c->path != 0, KM_ERR_UNSUPPORTED,
              "km_assign_stats: no kernel for d=" + std::to_string(c->g.d) + " (supported: d <= 2048)");
   KM_HIP(hipSetDevice(c->device));
+  int rc = flush_assign(c);
+  if (rc != KM_OK) return rc;
+  if (fold_ok(c)) {
+    // launched by km_update_async together with the update
+    if (c->prep_of != c->C64_cur) {
+      rc = prep(c);
+      if (rc != KM_OK) return rc;
+    }
+    c->assign_pending = true;
+    return KM_OK;
+  }
   return run_assign(c, true);
 }
 
 int km_stats_buffer(km_ctx* c, void** p, int64_t* len) {
   KM_REQUIRE(c && c->have_c && p && len, KM_ERR_STATE, "km_stats_buffer: set centroids first");
+  {
+    const int rc = flush_assign(c);
+    if (rc != KM_OK) return rc;
+  }
+  c->stats_exported = true;
   *p = c->stats;
   *len = (int64_t)stats_len(c->g);
   return KM_OK;
@@ -727,6 +793,10 @@ int km_stats_buffer(km_ctx* c, void** p, int64_t* len) {
 
 int km_bind_stats_buffer(km_ctx* c, void* p) {
   KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_bind_stats_buffer: set centroids first");
+  {
+    const int rc = flush_assign(c);
+    if (rc != KM_OK) return rc;
+  }
   c->stats = p ? reinterpret_cast<double*>(p) : c->stats_own;
   c->stats_clean = false;
   return KM_OK;
@@ -759,6 +829,10 @@ int km_update(km_ctx* c, km_status* st, int64_t* counts) {
   KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_update: set centroids first");
   KM_REQUIRE(!c->in_batch, KM_ERR_STATE, "km_update: inside a batch (use km_update_async)");
   KM_HIP(hipSetDevice(c->device));
+  {
+    const int rcf = flush_assign(c);
+    if (rcf != KM_OK) return rcf;
+  }
   {
     ProfScope ps(c, KM_K_UPDATE);
     KM_HIP(km::launch_update(c->stats, c->C64_cur, c->g, c->C64_new, c->work, c->counts_dev, c->qcount,
@@ -854,6 +928,30 @@ int km_update_async(km_ctx* c, double tol, int64_t empty_seed) {
   // no repair behind it, writes the next assign's centroid images itself
   const bool one = km::update_one_ok(c->g);
   const bool fold_prep = one && c->path == 1 && !repair;
+  if (c->assign_pending) {
+    // one launch: assign + sums + queued rows + update (last workgroup)
+    c->assign_pending = false;
+    c->ql = km::QLayout{0, 0};
+    if (!c->stats_clean) KM_HIP(hipMemsetAsync(c->stats, 0, sizeof(double) * stats_len(c->g), c->stream));
+    km::SmallTail t = small_tail(c);
+    t.fold = 1;
+    t.old = c->C64_cur;
+    t.out = c->C64_new;
+    t.counts = c->hist_counts + (size_t)slot * c->g.k;
+    t.st = c->hist + slot;
+    t.gate = c->gate;
+    t.stop_tol = tol;
+    t.dev_repair = 0;
+    t.C32n = fold_prep ? c->C32 : nullptr;
+    t.cmaxn = fold_prep ? c->cmax : nullptr;
+    {
+      ProfScope ps(c, KM_K_ASSIGN);
+      KM_HIP(km::launch_assign_small(c->X, c->g, c->C32, c->C64_cur, c->cmax, c->labels, c->stats, 1,
+                                     c->want_sse ? 1 : 0, c->n_cu, c->gate, c->stream, t));
+    }
+    c->stats_clean = true;  // the update cleared them
+    return finish_update(c, slot, fold_prep);
+  }
   {
     ProfScope ps(c, KM_K_UPDATE);
     KM_HIP(km::launch_update(c->stats, c->C64_cur, c->g, c->C64_new, c->work,
@@ -949,6 +1047,10 @@ int km_batch_end(km_ctx* c, km_status* st, int64_t* counts, int32_t* n_ran) {
   KM_REQUIRE(c && c->in_batch, KM_ERR_STATE, "km_batch_end: no open batch");
   KM_REQUIRE(n_ran, KM_ERR_ARG, "km_batch_end: null n_ran");
   KM_HIP(hipSetDevice(c->device));
+  {
+    const int rcf = flush_assign(c);
+    if (rcf != KM_OK) return rcf;
+  }
   const int m = c->batch_n;
   if (m > 0) {
     KM_HIP(hipMemcpyAsync(c->hist_host, c->hist, sizeof(km::DevStatus) * m, hipMemcpyDeviceToHost, c->stream));
@@ -1016,6 +1118,10 @@ int km_replace_rows(km_ctx* c, const int32_t* ids, const double* rows, int32_t n
   KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_replace_rows: set centroids first");
   KM_REQUIRE(n >= 0 && (n == 0 || (ids && rows)), KM_ERR_ARG, "km_replace_rows: bad args");
   KM_HIP(hipSetDevice(c->device));
+  {
+    const int rcf = flush_assign(c);
+    if (rcf != KM_OK) return rcf;
+  }
   if (n == 0) return KM_OK;
   if (c->prep_of == c->C64_new) c->prep_of = nullptr;  // its images are stale now
   c->screen = c->screen_forced >= 0 ? c->screen_forced : km::KM_SCREEN_X3_REFINE;
@@ -1040,6 +1146,10 @@ int km_replace_rows(km_ctx* c, const int32_t* ids, const double* rows, int32_t n
 int km_commit(km_ctx* c) {
   KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_commit: set centroids first");
   KM_HIP(hipSetDevice(c->device));
+  {
+    const int rcf = flush_assign(c);
+    if (rcf != KM_OK) return rcf;
+  }
   std::swap(c->C64_cur, c->C64_new);
   return c->prep_of == c->C64_cur ? KM_OK : prep(c);
 }
@@ -1051,6 +1161,10 @@ int km_gather_rows(km_ctx* c, const int64_t* idx, int32_t n, double* out) {
   for (int i = 0; i < n; ++i)
     KM_REQUIRE(idx[i] >= 0 && idx[i] < c->g.n, KM_ERR_ARG, "km_gather_rows: index out of range");
   KM_HIP(hipSetDevice(c->device));
+  {
+    const int rcf = flush_assign(c);
+    if (rcf != KM_OK) return rcf;
+  }
   int rc = ensure_scratch(c, n);
   if (rc != KM_OK) return rc;
   KM_HIP(hipMemcpyAsync(c->idx_scratch, idx, sizeof(int64_t) * n, hipMemcpyHostToDevice, c->stream));
@@ -1116,6 +1230,10 @@ int km_predict(km_ctx* c, int32_t* labels_out) {
   KM_REQUIRE(c && c->have_c, KM_ERR_STATE, "km_predict: set centroids first");
   KM_REQUIRE(c->path != 0, KM_ERR_UNSUPPORTED, "km_predict: unsupported geometry");
   KM_HIP(hipSetDevice(c->device));
+  {
+    const int rcf = flush_assign(c);
+    if (rcf != KM_OK) return rcf;
+  }
   int rc = run_assign(c, false);
   if (rc != KM_OK) return rc;
   if (labels_out && c->g.n > 0)
@@ -1127,6 +1245,10 @@ int km_predict(km_ctx* c, int32_t* labels_out) {
 int km_labels(km_ctx* c, int32_t* labels_out) {
   KM_REQUIRE(c && c->loaded && labels_out, KM_ERR_STATE, "km_labels: no data");
   KM_HIP(hipSetDevice(c->device));
+  {
+    const int rcf = flush_assign(c);
+    if (rcf != KM_OK) return rcf;
+  }
   if (c->g.n > 0)
     KM_HIP(hipMemcpyAsync(labels_out, c->labels, sizeof(int32_t) * c->g.n, hipMemcpyDeviceToHost, c->stream));
   KM_HIP(hipStreamSynchronize(c->stream));
