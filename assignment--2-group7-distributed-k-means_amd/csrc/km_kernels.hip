@@ -278,10 +278,11 @@ __device__ void update_one_body(double* __restrict__ stats, const double* __rest
                                 int* __restrict__ gate, double stop_tol, int dev_repair, int clear,
                                 float* __restrict__ C32, float* __restrict__ cmax, int dp, int kp);
 
-// 8 waves per SIMD at dp = 16 (c2: 32 VGPRs of row and prefetch), the
-// compiler's choice above (a row and its prefetch are 2 dp VGPRs)
+// waves per SIMD at dp = 16 (KM_SMALL_WPE; c2 on one MI355X: 4 waves with the
+// row prefetch 146-147 us, 8 waves without it 154-161 us), the compiler's
+// choice above (a row and its prefetch are 2 dp VGPRs)
 #ifndef KM_SMALL_WPE
-#define KM_SMALL_WPE 8
+#define KM_SMALL_WPE 4
 #endif
 template <int DP, bool SSE, int WPE = (DP <= 16 ? KM_SMALL_WPE : 1)>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
@@ -541,7 +542,13 @@ int diag_env(const char* name, int dflt) {
 
 // statistics replicas: as many as fit the LDS share of one of the 8
 // workgroups a CU holds at 8 waves per SIMD (20 KiB each), at most 32
-static constexpr int SMALL_WG_LDS = 20 * 1024;
+#ifndef KM_SMALL_LDS
+#define KM_SMALL_LDS (20 * 1024)
+#endif
+#ifndef KM_SMALL_BPC
+#define KM_SMALL_BPC 8
+#endif
+static constexpr int SMALL_WG_LDS = KM_SMALL_LDS;
 static int small_replicas(const Geometry& g) {
   const size_t cbytes = ((size_t)g.k * g.dp * 4 + 15) / 16 * 16;
   static const int rmax = diag_env("KM_SMALL_R", 32);
@@ -566,7 +573,7 @@ hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C
   const size_t lds = ((size_t)g.k * g.dp * 4 + 15) / 16 * 16 + (fuse ? (size_t)g.k * (g.d + 1) * 8 * R : 0) +
                      (size_t)4 * SMALL_QW * 4;
   int64_t blocks = (g.n + 255) / 256;
-  static const int bpc = diag_env("KM_SMALL_BPC", 8);
+  static const int bpc = diag_env("KM_SMALL_BPC", KM_SMALL_BPC);
   const int64_t cap = (int64_t)n_cu * bpc;
   if (blocks > cap) blocks = cap;
 #define KM_SMALL_CASE(DP_)                                                                                 \

@@ -103,22 +103,6 @@ def usable_cpus():
     return max(1, n)
 
 
-def power_floor(config, n_local, n_total):
-    """The fp16x3 MFMA work of the fused kernel alone (ablation ABL=5: MFMAs,
-    split and row loads; no keys, merge, queue or sums), from the committed SQ
-    counter pass (profiles/r3_c3_sq_ablations.json), scaled to this rank's rows."""
-    path = os.path.join(ROOT, "profiles", "r3_c3_sq_ablations.json")
-    if config not in ("c3", "c3_shard8", "c3_small") or not os.path.exists(path):
-        return None
-    try:
-        v = json.load(open(path))["variants"]["abl5"]["mean"]
-    except (OSError, ValueError, KeyError):
-        return None
-    return {"ms": v["duration_ms"] * n_local / CONFIGS["c3"][0], "clock_ghz": v["clock_ghz"],
-            "mfma_busy": v["mfma_busy_per_simd"],
-            "source": "profiles/r3_c3_sq_ablations.json abl5 (N=100M, scaled by rows)"}
-
-
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -255,7 +239,10 @@ def main():
                     "peak_note": f"dense f16 MFMA 2516.6 TF; achieved = {nx}*2*n*k*d per launch / avg launch time"}
     elif info["path"] == 2 and dom == "assign":
         ach = flops_launch / avg_s / 1e12
-        kname = ("k_fused (fp16x3 screen + f64 sums)" if info["fused_stats"] else
+        # the fused screen runs on v_mfma_f32_16x16x32_f16 where dp is a
+        # multiple of 32 (k_fused16), else on 32x32x16 (k_fused)
+        kname = (("k_fused16 (fp16x3 screen on 16x16x32 MFMA + f64 sums)" if info["dp"] % 32 == 0 else
+                  "k_fused (fp16x3 screen on 32x32x16 MFMA + f64 sums)") if info["fused_stats"] else
                  "k_assign_wide (fp16x3 screen, feature chunks)" if info["dp"] > 256 else
                  "k_assign_mfma (fp16x3 screen)")
         roof = {"bound": "mfma", "achieved": ach, "peak": F16X3_EFFECTIVE_TFLOPS, "unit": "TFLOP/s",
@@ -263,11 +250,6 @@ def main():
                 "peak_note": "dense f16 MFMA 2516.6 TF / 3 (fp16x3 split: 3 MFMAs per product); "
                              "achieved = 2*n*k*d per launch / avg launch time (HIP events, engine stream)",
                 "hbm_gbs": n_local * d * 4 / avg_s / 1e9}
-        floor = power_floor(args.config, n_local, N)
-        if floor is not None and info["fused_stats"]:
-            # measured ceiling of the same MFMA work under the chip's power
-            # management ("The c3 screen is power-bound")
-            roof["power_floor"] = dict(floor, frac_of_floor=floor["ms"] / (avg_s * 1e3))
     else:
         b = bytes_stats if dom == "stats" else bytes_assign
         ach = b / avg_s / 1e9

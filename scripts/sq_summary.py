@@ -30,6 +30,10 @@ for disp in sorted(per):
                  "active_inst_any": raw["SQ_ACTIVE_INST_ANY"] / wc, "active_inst_valu": raw["SQ_ACTIVE_INST_VALU"] / wc,
                  "wait_inst_any": raw["SQ_WAIT_INST_ANY"] / wc, "wait_any": raw["SQ_WAIT_ANY"] / wc,
                  "raw": dict(raw)})
+# gated no-op dispatches (a stopped batch's later launches) are left out, as
+# in scripts/trace_summary.py: shorter than 1% of the longest dispatch
+longest = max(r["duration_ms"] for r in rows)
+rows = [r for r in rows if r["duration_ms"] >= 0.01 * longest]
 mean = {k: sum(r[k] for r in rows) / len(rows) for k in rows[0] if k not in ("dispatch", "raw")}
 json.dump({"kernel": f"{kname} (c3)",
            "source": "rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY "
