@@ -152,8 +152,10 @@ size_t sorted_stats_words(int64_t n, int k);
 hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t* labels, double* stats,
                                uint32_t* scratch, const double* C64P, int n_cu, const int* gate, hipStream_t s);
 // C64P != nullptr: the SSE residuals are accumulated in the same pass
+// C64P, C32 != nullptr: the SSE residuals in the same pass (to the fp32 image,
+// corrected per cluster to the float64 centroid at the flush)
 hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels, double* stats, int n_cu,
-                        const int* gate, hipStream_t s, const double* C64P = nullptr);
+                        const int* gate, hipStream_t s, const double* C64P = nullptr, const float* C32 = nullptr);
 // stats = [k][d+1] sums and counts, then the SSE slot stats[k (d+1)]
 // gate: the batch's stop flag (kernels of later iterations no-op once it is
 // set); stop_tol >= 0 lets k_finalize raise it (KM_STOP_*), < 0 never

@@ -438,10 +438,8 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
           take = (on && !mn) || (on == mn && (on ? oj < j : (ov < v || (ov == v && oj < j))));
         }
       }
-      if (take) {
-        v = ov;
-        j = oj;
-      }
+      v = take ? ov : v;  // select form
+      j = take ? oj : j;
     }
     const int lab = j < 0 ? 0 : j;
     if (lane == 0) {
@@ -3778,14 +3776,14 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
       else
         np_pw8<2>(sq2, 0, d, u, sa, sb);
       const double va = sqrt(sa), vb = sqrt(sb);
-      if (np_better(va, mnorm, bi >= 0)) {
-        mnorm = va;
-        bi = a;
-      }
-      if (bb != a && np_better(vb, mnorm, true)) {
-        mnorm = vb;
-        bi = bb;
-      }
+      // running minimum updated with selects (the
+      // branchy form is miscompiled in divergent code on this toolchain)
+      const bool ua = np_better(va, mnorm, bi >= 0);
+      mnorm = ua ? va : mnorm;
+      bi = ua ? a : bi;
+      const bool ub = bb != a && np_better(vb, mnorm, true);
+      mnorm = ub ? vb : mnorm;
+      bi = ub ? bb : bi;
     }
     lab = bi < 0 ? 0 : bi;
     if (!have) continue;
@@ -3796,10 +3794,9 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
       for (int j = 0; j < k; ++j) {
         const double* __restrict__ c = C64 + (size_t)j * d;
         const double v = np_norm_d<WIDE ? 5 : 2>([&](int f) { return np_sq(c[f], x[f]); }, d);
-        if (np_better(v, best, j > 0)) {
-          best = v;
-          lab = j;
-        }
+        const bool u = np_better(v, best, j > 0);  // select form
+        best = u ? v : best;
+        lab = u ? j : lab;
       }
       rsq_bad = best;  // the norm (np_norm_d takes the sqrt)
     }
@@ -3945,10 +3942,8 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
             take = (on && !mn) || (on == mn && (on ? oj < bi : (ob < bv || (ob == bv && oj < bi))));
           }
         }
-        if (take) {
-          bv = ob;
-          bi = oj;
-        }
+        bv = take ? ob : bv;  // select form
+        bi = take ? oj : bi;
       }
       const int lab = bi < 0 ? 0 : bi;
       if (lane == 0) labels[rows[g]] = lab;
@@ -3997,10 +3992,9 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
       for (int j = chain[g] + 8 * lane; j < k; j += 8 * 64) {
         const float* xg = xs + g * d;
         const double v = np_norm_d<2>([&](int f) { return np_sq(C64T[(size_t)f * k + j], xg[f]); }, d);
-        if (np_better(v, bv, bi >= 0)) {
-          bv = v;
-          bi = j;
-        }
+        const bool u = np_better(v, bv, bi >= 0);  // select form
+        bv = u ? v : bv;
+        bi = u ? j : bi;
       }
       finish(g, bv, bi);
       have[g] = false;
@@ -4023,10 +4017,9 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
       static_assert(G == 2 || G == 4, "entries per wave");
       auto direct = [&](int j, const float* xg, double& bst, int& bjj) {
         const double v = np_norm_d<5>([&](int f) { return np_sq(C64T[(size_t)f * k + j], xg[f]); }, d);
-        if (np_better(v, bst, bjj >= 0)) {
-          bst = v;
-          bjj = j;
-        }
+        const bool u = np_better(v, bst, bjj >= 0);  // select form
+        bst = u ? v : bst;
+        bjj = u ? j : bjj;
       };
       for (int j = lane; j < k; j += 64) {
         if (have[0]) direct(j, xs, best[0], bj[0]);
@@ -4147,12 +4140,14 @@ static constexpr int STATS_LDS = 156 * 1024;
 // k (d+1) doubles exceed LDS but k (fr+1) fit (c4: 1024 clusters x 16 features).
 // PLAIN (diagnostic build, KM_ABLATE=14): LDS read-add-write instead of the
 // float64 LDS atomics (races: results wrong by design), to price the atomics
-template <bool PLAIN = false>
+template <bool PLAIN = false, bool SSE = false>
 __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int64_t n, int d, int dp, int k,
                                                 const int32_t* __restrict__ labels, double* __restrict__ stats,
                                                 int kr, int fr, int64_t rows_per_block, const double* __restrict__ C64P,
-                                                double* __restrict__ sse, const int* __restrict__ gate) {
+                                                const float* __restrict__ C32, double* __restrict__ sse,
+                                                const int* __restrict__ gate) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
+  if constexpr (!SSE) sse = nullptr;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* tab = reinterpret_cast<double*>(smem);
   // LDS row of a cluster: fr feature slots + count.  Feature f0 + 4m + c is
@@ -4163,7 +4158,7 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
   const int c0 = blockIdx.y * kr;
   const int c1 = min(k, c0 + kr);
   const int f0 = blockIdx.z * fr;
-  const bool counts = blockIdx.z == 0;
+  const bool counts = blockIdx.z == 0;  // the count column reaches the global statistics from range 0 only
   const int nent = (c1 - c0) * RS;
   for (int i = threadIdx.x; i < nent; i += blockDim.x) tab[i] = 0.0;
   __syncthreads();
@@ -4178,17 +4173,22 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
   // L not dividing 64 (fr = 48, 96, 152, 196, ...): the lanes past the last
   // whole row idle (lane q = P would repeat row u + 1's first features)
   const bool act = q < P;
-  constexpr int U = 8;         // float4 loads in flight per lane
+  constexpr int U = SSE ? 6 : 8;  // float4 rows in flight per lane (SSE: and as many centroid images)
   // SSE (compute_sse, kmeans_spark.py:224-237) in the same pass: each
   // (row, feature range) is summed by exactly one workgroup (the one owning
-  // the row's cluster), which adds the range's float64 residual to the
-  // row's pre-update centroid (C64P, L2-resident, gathered by label); the
-  // ranges' partial residuals sum to the row's
+  // the row's cluster).  Per row it adds the float64 residual to the fp32
+  // image c' of the pre-update centroid (C32, 16 B per 4 features gathered
+  // from L2 instead of C64P's 32 B); at the flush it corrects to the float64
+  // centroid c = c' + delta per cluster and feature, exactly in algebra:
+  //   sum_rows (x - c)^2 = sum_rows (x - c')^2 - 2 delta (S - n c') + n delta^2
+  // with S, n this workgroup's own partial sums and count (linear, so the
+  // workgroups' corrections add up).  |delta| <= 2^-24 |c|, so the
+  // correction's own rounding is ~2^-75 n |c|^2
   double ss = 0.0;
   for (int64_t cr = r0 + (int64_t)wave * 64; cr < r1; cr += (int64_t)nwaves * 64) {
     const int nrow = (int)min((int64_t)64, r1 - cr);
     const int labreg = lane < nrow ? labels[cr + lane] : -1;
-    if (counts && lane < nrow && labreg >= c0 && labreg < c1) atomicAdd(tab + (labreg - c0) * RS + fr, 1.0);
+    if ((counts || sse) && lane < nrow && labreg >= c0 && labreg < c1) atomicAdd(tab + (labreg - c0) * RS + fr, 1.0);
     const float* base = X + cr * dp + f0;
     for (int rb = 0; rb < nrow; rb += P * U) {
       float4 v[U];
@@ -4198,10 +4198,25 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
         v[u] = (act && rr < nrow) ? *reinterpret_cast<const float4*>(base + (size_t)rr * dp + 4 * mm)
                                   : make_float4(0.f, 0.f, 0.f, 0.f);
       }
+      // the rows' labels, then (SSE) every row's centroid image gathered
+      // before any is used: U L2 loads in flight instead of U dependent ones
+      int labs[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) labs[u] = __shfl(labreg, (rb + u * P + q) & 63);
+      float4 cg[U];
+      if (sse) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int rr = rb + u * P + q;
+          const bool mine = act && rr < nrow && labs[u] >= c0 && labs[u] < c1;
+          cg[u] = mine ? *reinterpret_cast<const float4*>(C32 + (size_t)labs[u] * dp + f0 + 4 * mm)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int rr = rb + u * P + q;
-        const int lab = __shfl(labreg, rr & 63);
+        const int lab = labs[u];
         if (act && rr < nrow && lab >= c0 && lab < c1) {
           double* t = tab + (lab - c0) * RS + mm;
           if constexpr (PLAIN) {
@@ -4216,11 +4231,9 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
             atomicAdd(t + 3 * L, (double)v[u].w);
           }
           if (sse) {  // padded features are 0 - 0
-            const double* c = C64P + (size_t)lab * dp + f0 + 4 * mm;
-            const double2 ca = *reinterpret_cast<const double2*>(c);
-            const double2 cb = *reinterpret_cast<const double2*>(c + 2);
-            const double t0 = (double)v[u].x - ca.x, t1 = (double)v[u].y - ca.y;
-            const double t2 = (double)v[u].z - cb.x, t3 = (double)v[u].w - cb.y;
+            const float4 c = cg[u];
+            const double t0 = (double)v[u].x - (double)c.x, t1 = (double)v[u].y - (double)c.y;
+            const double t2 = (double)v[u].z - (double)c.z, t3 = (double)v[u].w - (double)c.w;
             ss = fma(t0, t0, ss);
             ss = fma(t1, t1, ss);
             ss = fma(t2, t2, ss);
@@ -4230,25 +4243,36 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
       }
     }
   }
-  if (sse) {
-    ss = wave_sum(ss);
-    if (lane == 0 && ss != 0.0) atomicAdd(sse, ss);
-  }
   __syncthreads();
   const int d1 = d + 1;
   for (int i = threadIdx.x; i < nent; i += blockDim.x) {
     const int j = i / RS;
     const int p = i - j * RS;
     const double v = tab[i];
-    if (v == 0.0) continue;
     int f;
     if (p == fr) {
-      f = d;  // count (feature range 0 only)
+      if (!counts) continue;  // counts only from feature range 0
+      f = d;
     } else {
       f = f0 + 4 * (p % L) + p / L;
       if (f >= d) continue;  // zero padding
+      if (sse) {
+        // delta (S - n c') and n delta^2 of this (cluster, feature); a zero
+        // sum S still has a correction when n > 0
+        const double n = tab[j * RS + fr];
+        if (n != 0.0) {
+          const double cp = (double)C32[(size_t)(c0 + j) * dp + f];
+          const double dl = C64P[(size_t)(c0 + j) * dp + f] - cp;
+          ss += dl * (n * dl - 2.0 * (v - n * cp));
+        }
+      }
     }
+    if (v == 0.0) continue;
     atomicAdd(stats + (size_t)(c0 + j) * d1 + f, v);
+  }
+  if (sse) {
+    ss = wave_sum(ss);
+    if (lane == 0 && ss != 0.0) atomicAdd(sse, ss);
   }
 }
 
@@ -4289,8 +4313,9 @@ static void stats_ranges(const Geometry& g, int* fr_out, int* kr_out) {
 }
 
 hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels, double* stats, int n_cu,
-                        const int* gate, hipStream_t s, const double* C64P) {
+                        const int* gate, hipStream_t s, const double* C64P, const float* C32) {
   if (g.n == 0) return hipSuccess;
+  if (C64P && !C32) return hipErrorInvalidValue;
   if (g.dp > WIDE_MAX_DP || g.dp % 4) return hipErrorInvalidValue;
   int fr = 0, kr = 0;
   stats_ranges(g, &fr, &kr);
@@ -4310,15 +4335,19 @@ hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels
 #ifdef KM_DIAG
   static const int abl = diag_env("KM_ABLATE", 0);
   if (abl == 14) {
-    hipLaunchKernelGGL(k_stats<true>, dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024), lds, s, X,
-                       g.n, g.d, g.dp, g.k, labels, stats, kr, fr, rpb, C64P,
+    hipLaunchKernelGGL((k_stats<true, false>), dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024), lds, s, X,
+                       g.n, g.d, g.dp, g.k, labels, stats, kr, fr, rpb, C64P, C32,
                        C64P ? stats + (size_t)g.k * (g.d + 1) : (double*)nullptr, gate);
     return hipGetLastError();
   }
 #endif
-  hipLaunchKernelGGL(k_stats<false>, dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024), lds, s, X,
-                     g.n, g.d, g.dp, g.k, labels, stats, kr, fr, rpb, C64P,
-                     C64P ? stats + (size_t)g.k * (g.d + 1) : (double*)nullptr, gate);
+  if (C64P)
+    hipLaunchKernelGGL((k_stats<false, true>), dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024), lds,
+                       s, X, g.n, g.d, g.dp, g.k, labels, stats, kr, fr, rpb, C64P, C32,
+                       stats + (size_t)g.k * (g.d + 1), gate);
+  else
+    hipLaunchKernelGGL((k_stats<false, false>), dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024),
+                       lds, s, X, g.n, g.d, g.dp, g.k, labels, stats, kr, fr, rpb, C64P, C32, (double*)nullptr, gate);
   return hipGetLastError();
 }
 

@@ -451,7 +451,8 @@ int run_assign(km_ctx* c, bool with_stats) {
                                      c->n_cu, c->gate, c->stream));
     } else {
       // SSE residuals in the same pass over X (feature-range tiles)
-      KM_HIP(km::launch_stats(c->X, g, c->labels, c->stats, c->n_cu, c->gate, c->stream, sse ? c->C64P : nullptr));
+      KM_HIP(km::launch_stats(c->X, g, c->labels, c->stats, c->n_cu, c->gate, c->stream, sse ? c->C64P : nullptr,
+                              sse ? c->C32 : nullptr));
     }
   }
   return KM_OK;

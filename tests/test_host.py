@@ -766,3 +766,10 @@ def test_fullscan_lockstep_updates_minima_with_selects():
     assert "np_pw2<2>(" in body
     assert "best[g + 1] = ub ? vb : best[g + 1];" in body
     assert re.search(r"if \(have\[g \+ 1\] && np_better", body) is None
+    # the same defect class everywhere (the structurized
+    # branch's copy for the not-taken lanes runs for every lane that reached
+    # the comparison): no running minimum or argmin shuffle is updated under
+    # an if in any kernel
+    code = re.sub(r"//[^\n]*", "", src)
+    assert re.search(r"if \([^;{]*np_better\(", code) is None
+    assert re.search(r"if \(take\)", code) is None
