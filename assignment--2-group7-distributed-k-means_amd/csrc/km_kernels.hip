@@ -2449,898 +2449,12 @@ __global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Software-pipelined fused kernel (the c3 class with statistics, no SSE): the
-// same screen, bound, labels, queue and float64 sums as k_fused, arranged so
-// that one wave per SIMD keeps the matrix pipe busy.  In k_fused a tile's
-// split, merge and 33 LDS atomics run between MFMA blocks, serialised with
-// them (MFMA busy 49%, VALU 44%).  Here, while the MFMAs
-// of tile t run:
-//   * the sums of tile t-1 fill the gaps of the first half of the blocks: the
-//     rows of tile t-1 are re-read (L2-resident: loaded one tile earlier)
-//     instead of being held in 32 VGPRs, their loads issued before the next
-//     tile's HBM loads so the in-order vmcnt lets those stay in flight;
-//     rows that are not summed here (queued for the resolvers, or past the
-//     end) add into a discard column KP of the table, so the region has no
-//     branch (a branch would end the scheduling region);
-//   * the split of tile t+1 fills the gaps of the second half, into the
-//     other of two ping-pong B-operand sets.
-// What stays between blocks is the last block's keys and the merge / bound /
-// label / queue of tile t.
-// Diagnostic build only (KM_ABLATE=10; 9 with phase stamps): parity-green, but
-// no faster than k_fused in A/B/A runs on one box (11.2 ms both, DESIGN.md
-// section 4) -- the c3 screen is at its power floor, not schedule-bound.
-// ---------------------------------------------------------------------------
+// The diagnostic build's experimental kernels -- k_fusedp (software-pipelined
+// fused kernel) and the fast screen k_fused1 / k_prep_bal -- live in
+// km_diag.inc, compiled only by `make diag`.
 #ifdef KM_DIAG
-// STAMP (diagnostic build, KM_ABLATE=9): s_memtime phase stamps per tile
-// (head = loads + block 0, region = blocks 1 .. NB-1, tail = last keys +
-// merge + queue), the wave's whole-kernel cycles and s_memrealtime ticks
-template <int NS, int NB, bool REF, bool STAMP = false>
-__global__ __launch_bounds__(256, 1) void k_fusedp(FusedArgs A) {
-  if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
-  constexpr int DP = 16 * NS;
-  constexpr int KP = 32 * NB;
-  constexpr int WAVES = 4;
-  constexpr int B = ceil_log2_c(KP);
-  static_assert(B >= 3 && B - 2 <= 12, "index bits");
-  static_assert(NB >= 2, "pipelined blocks");
-  constexpr uint32_t maskq = (1u << (B - 2)) - 1u;
-  constexpr int TS = KP + 1;  // sum table row stride: column KP discards
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* sCn = reinterpret_cast<float*>(smem);              // ||c||^2 s^2 [KP]
-  double* tab = reinterpret_cast<double*>(smem + KP * 4);   // [DP + 1][TS]
-
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int r = lane & 31;
-  const int h = lane >> 5;
-  for (int i = threadIdx.x; i < KP; i += WAVES * 64) sCn[i] = A.cn2s[i];
-  for (int i = threadIdx.x; i < (DP + 1) * TS; i += WAVES * 64) tab[i] = 0.0;
-  f16x8 Ahi[NB][NS], Alo[NB][NS];
-#pragma unroll
-  for (int b = 0; b < NB; ++b)
-#pragma unroll
-    for (int t = 0; t < NS; ++t) {
-      Ahi[b][t] = __builtin_bit_cast(f16x8, A.ChiF[(b * NS + t) * 64 + lane]);
-      Alo[b][t] = __builtin_bit_cast(f16x8, A.CloF[(b * NS + t) * 64 + lane]);
-    }
-#pragma unroll
-  for (int b = 0; b < NB; ++b)
-#pragma unroll
-    for (int t = 0; t < NS; ++t) asm volatile("" : "+a"(Ahi[b][t]), "+a"(Alo[b][t]));
-  __syncthreads();
-
-  const float s = mfma_scale(*A.xabs, *A.cabs);
-  const float alpha = A.bnd[0], beta = A.bnd[1];
-  const float rho = __builtin_ldexpf(1.0f, B - 2 - 23) * 1.01f;
-  const int64_t n = A.n;
-  const int64_t ntiles = (n + 31) / 32;
-  const uint32_t gw = blockIdx.x * WAVES + wave;
-  QEntry* wq = A.queue + (size_t)gw * A.seg;
-  uint32_t qn = 0, qf = 0;
-  const int64_t tstride = (int64_t)gridDim.x * WAVES;
-  const float4* cnl = reinterpret_cast<const float4*>(sCn + 4 * h);
-
-  // rows of a tile (clamped to row n - 1 past the end: every path has the
-  // same loads in flight)
-  auto load_rows = [&](int64_t tile, float4 (&xq)[NS][2]) {
-    const int64_t row = tile * 32 + r;
-    const int64_t rr = row < n ? row : (n - 1);
-    const float* xr = A.X + rr * DP + 8 * h;
-#pragma unroll
-    for (int t = 0; t < NS; ++t) {
-      xq[t][0] = *reinterpret_cast<const float4*>(xr + 16 * t);
-      xq[t][1] = *reinterpret_cast<const float4*>(xr + 16 * t + 4);
-    }
-  };
-  auto load_xn = [&](int64_t tile) {
-    const int64_t row = tile * 32 + r;
-    return A.xnorm[row < n ? row : (n - 1)];
-  };
-  // B operand chunk t: lane (r, h) holds features [16t + 8h, +8) of point r,
-  // xs = hi + lo (fp16, RN), one v_fma_mix per element for lo (as k_fused)
-  auto split_chunk = [&](const float4 (&xq)[NS][2], int t, f16x8& bh, f16x8& bl) {
-    // opaque copies: otherwise the vectoriser hoists the x * s products next
-    // to the loads, which then wait for HBM at the top of the tile
-    float xv[8] = {xq[t][0].x, xq[t][0].y, xq[t][0].z, xq[t][0].w,
-                   xq[t][1].x, xq[t][1].y, xq[t][1].z, xq[t][1].w};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) asm("" : "+v"(xv[e]));
-#pragma unroll
-    for (int e = 0; e < 8; e += 2) {
-      const float xs0 = xv[e] * s, xs1 = xv[e + 1] * s;
-      const f16x2 hp = {(_Float16)xs0, (_Float16)xs1};
-      const f16x2 lo = split_lo(hp, xs0, xs1);
-      bh[e] = hp[0];
-      bh[e + 1] = hp[1];
-      bl[e] = lo[0];
-      bl[e + 1] = lo[1];
-    }
-  };
-  // sums of chunk t of the previous tile: 8 features of its row into the
-  // table column plab (KP: discard)
-  auto sum_chunk = [&](const float4 (&xq)[NS][2], int t, int plab) {
-    double* tp = tab + (size_t)(16 * t + 8 * h) * TS + plab;
-    const float xe[8] = {xq[t][0].x, xq[t][0].y, xq[t][0].z, xq[t][0].w,
-                         xq[t][1].x, xq[t][1].y, xq[t][1].z, xq[t][1].w};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      // the conversion through inline asm: as plain (double) the vectoriser
-      // hoists all 32 conversions next to the loads (64 more live VGPRs and
-      // a vmcnt(0) in front of the next tile's HBM loads)
-      double v;
-      asm("v_cvt_f64_f32 %0, %1" : "=v"(v) : "v"(xe[e]));
-      atomicAdd(tp + (size_t)e * TS, v);
-    }
-  };
-
-  // the tile's B operands (ping-pong), the next tile's rows, previous tile
-  f16x8 bA[NS], lA[NS], bB[NS], lB[NS];
-  float4 xnext[NS][2];
-  float xnA = 0.0f, xnB = 0.0f;
-  int64_t prow = (int64_t)gw * 32 + r;  // re-read address of the previous tile's row (clamped)
-  int plab = KP;                        // previous tile: column summed into (KP: discard)
-  int pcnt = KP;                        // count column (h == 0 lanes only), KP: discard
-  unsigned long long st_acc[3] = {0, 0, 0}, st_t = 0;
-  const unsigned long long st_k0 = STAMP ? __builtin_amdgcn_s_memtime() : 0;
-  const unsigned long long st_r0 = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
-  auto stamp = [&](int slot) {
-    if constexpr (STAMP) {
-      __builtin_amdgcn_sched_barrier(0);
-      const unsigned long long tn = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_sched_barrier(0);
-      if (slot >= 0) st_acc[slot] += tn - st_t;
-      st_t = tn;
-    }
-  };
-
-  auto tile_step = [&](int64_t tile, f16x8 (&bh)[NS], f16x8 (&bl)[NS], f16x8 (&bhn)[NS], f16x8 (&bln)[NS],
-                       float xn, float& xn_next) {
-    stamp(-1);
-    const int64_t row = tile * 32 + r;
-    const bool valid = row < n;
-    // previous tile's rows (L2), then the next tile's (HBM): the in-order
-    // vmcnt waits for the re-read alone
-    float4 xprev[NS][2];
-    {
-      const float* xr = A.X + (prow < n ? prow : (n - 1)) * DP + 8 * h;
-#pragma unroll
-      for (int t = 0; t < NS; ++t) {
-        xprev[t][0] = *reinterpret_cast<const float4*>(xr + 16 * t);
-        xprev[t][1] = *reinterpret_cast<const float4*>(xr + 16 * t + 4);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);  // keep the re-read older than the HBM loads
-    load_rows(tile + tstride, xnext);
-    xn_next = load_xn(tile + tstride);
-    __builtin_amdgcn_sched_barrier(0);
-
-    float a1[4], a2[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) a1[c] = a2[c] = FLT_MAX;
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int t = 0; t < NS; ++t) asm volatile("" : "+a"(Ahi[b][t]), "+a"(Alo[b][t]));
-    auto cn_init = [&](int blk) {
-      f32x16 acc;
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const float4 cv = cnl[8 * blk + 2 * g4];
-        acc[4 * g4 + 0] = cv.x;
-        acc[4 * g4 + 1] = cv.y;
-        acc[4 * g4 + 2] = cv.z;
-        acc[4 * g4 + 3] = cv.w;
-      }
-      return acc;
-    };
-    auto mfma_block = [&](f32x16 acc, int blk) {
-#pragma unroll
-      for (int t = 0; t < NS; ++t) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bl[t], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Alo[blk][t], bh[t], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bh[t], acc, 0, 0, 0);
-      }
-      return acc;
-    };
-    // one MFMA of block blk: step i = 3 t + (0: hi x lo, 1: lo x hi, 2: hi x hi)
-    auto mfma_step = [&](f32x16& acc, int blk, int i) {
-      const int t = i / 3, w = i % 3;
-      if (w == 0) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bl[t], acc, 0, 0, 0);
-      if (w == 1) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Alo[blk][t], bh[t], acc, 0, 0, 0);
-      if (w == 2) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bh[t], acc, 0, 0, 0);
-    };
-    // keys of one chain pair p of block blk (registers ra, ra + 4 of chain
-    // c): new best = min3(best, ka, kb), new second = min(second, med3(...));
-    // keys carry (j >> 2) without the lane-half bit h: 8 blk + 2 (reg >> 2),
-    // an inline constant for KP <= 256 (no index registers); h is put back
-    // in pidx.  Keys of the two halves can then tie exactly only between
-    // different centroids of equal truncated score, which leaves no
-    // certificate (k2 - k1 = 0): such a row is queued, its label and sums
-    // come from the resolvers, and every decision that sums a row here
-    // (kind 0) depends on the key values alone, identical in both halves
-    auto key_pair = [&](const f32x16& acc, int blk, int pp) {
-      const int c = pp & 3, ra = 8 * (pp >> 2) + c, rb = ra + 4;
-      const float ka = __uint_as_float((__float_as_uint(acc[ra]) & ~maskq) | (uint32_t)(8 * blk + 2 * (ra >> 2)));
-      const float kb = __uint_as_float((__float_as_uint(acc[rb]) & ~maskq) | (uint32_t)(8 * blk + 2 * (rb >> 2)));
-      const float tm = __builtin_amdgcn_fmed3f(a1[c], ka, kb);
-      a1[c] = __builtin_fminf(__builtin_fminf(a1[c], ka), kb);
-      a2[c] = __builtin_fminf(a2[c], tm);
-    };
-    auto cn_part = [&](f32x16& acc, int blk, int g4) {
-      const float4 cv = cnl[8 * blk + 2 * g4];
-      acc[4 * g4 + 0] = cv.x;
-      acc[4 * g4 + 1] = cv.y;
-      acc[4 * g4 + 2] = cv.z;
-      acc[4 * g4 + 3] = cv.w;
-    };
-    // One element pair (e, e+1) of chunk t: sums of the previous tile (two
-    // features into the table) or the split of the next tile
-    auto sum_pair = [&](int t, int e) {
-      double* tp = tab + (size_t)(16 * t + 8 * h + e) * TS + plab;
-      const float x0 = (e & 4) ? ((e & 2) ? xprev[t][1].z : xprev[t][1].x) : ((e & 2) ? xprev[t][0].z : xprev[t][0].x);
-      const float x1 = (e & 4) ? ((e & 2) ? xprev[t][1].w : xprev[t][1].y) : ((e & 2) ? xprev[t][0].w : xprev[t][0].y);
-      double v0, v1;
-      // the conversions through inline asm: as plain (double) the vectoriser
-      // hoists all 32 next to the loads (64 more live VGPRs, and a vmcnt(0)
-      // in front of the next tile's HBM loads)
-      asm("v_cvt_f64_f32 %0, %1" : "=v"(v0) : "v"(x0));
-      asm("v_cvt_f64_f32 %0, %1" : "=v"(v1) : "v"(x1));
-      atomicAdd(tp, v0);
-      atomicAdd(tp + TS, v1);
-    };
-    auto split_pair = [&](int t, int e) {
-      float x0 = (e & 4) ? ((e & 2) ? xnext[t][1].z : xnext[t][1].x) : ((e & 2) ? xnext[t][0].z : xnext[t][0].x);
-      float x1 = (e & 4) ? ((e & 2) ? xnext[t][1].w : xnext[t][1].y) : ((e & 2) ? xnext[t][0].w : xnext[t][0].y);
-      // opaque: otherwise the products are hoisted next to the HBM loads
-      asm("" : "+v"(x0));
-      asm("" : "+v"(x1));
-      const float xs0 = x0 * s, xs1 = x1 * s;
-      const f16x2 hp = {(_Float16)xs0, (_Float16)xs1};
-      const f16x2 lo = split_lo(hp, xs0, xs1);
-      bhn[t][e] = hp[0];
-      bhn[t][e + 1] = hp[1];
-      bln[t][e] = lo[0];
-      bln[t][e + 1] = lo[1];
-    };
-
-    // Explicit schedule of one block (M = 3 NS MFMAs, each followed by its
-    // filler work and a sched_barrier, so the issue order is the program
-    // order): key pair p of the previous block at step 2 + p (M - 4) / 8
-    // (the first two steps cover the previous block's MFMA latency); the
-    // next block's accumulator init, registers 4 g4 .. 4 g4 + 3, right after
-    // the last key pair that reads them; fillers at the other steps.  The
-    // tile's fillers -- NS sum chunks of the previous tile, then NS split
-    // chunks of the next -- are spread over blocks 2 .. NB-1 (sums first: the
-    // re-read needs an L2 round trip, the split waits for HBM).
-    constexpr int M = 3 * NS;
-    constexpr int F0 = NB >= 4 ? 2 : 1;  // first block with fillers
-    auto key_step = [&](int pp) { return 2 + (pp * (M - 4 > 0 ? M - 4 : 1)) / 8; };
-    f32x16 accs[2];
-    auto run_block = [&](int blk) {
-      f32x16& acc = accs[blk & 1];
-      f32x16& prev = accs[(blk - 1) & 1];
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        mfma_step(acc, blk, i);
-#pragma unroll
-        for (int pp = 0; pp < 8; ++pp)
-          if (key_step(pp) == i || (pp == 7 && i == M - 1 && key_step(7) >= M)) key_pair(prev, blk - 1, pp);
-        if (blk + 1 < NB) {
-          if (i == key_step(3) || (i == M - 1 && key_step(3) >= M)) {
-            cn_part(prev, blk + 1, 0);
-            cn_part(prev, blk + 1, 1);
-          }
-          if (i == key_step(7) || (i == M - 1 && key_step(7) >= M)) {
-            cn_part(prev, blk + 1, 2);
-            cn_part(prev, blk + 1, 3);
-          }
-        }
-        // filler slots: the steps without a key pair; chunk u of the tile's
-        // 2 NS filler chunks (4 element pairs each) belongs to block
-        // F0 + u (NB - F0) / (2 NS)
-        bool keyed = false;
-#pragma unroll
-        for (int pp = 0; pp < 8; ++pp) keyed |= key_step(pp) == i;
-        if (!keyed || M <= 6) {
-          int slot = 0, nslots = 0;
-#pragma unroll
-          for (int q = 0; q < M; ++q) {
-            bool kq = false;
-#pragma unroll
-            for (int pp = 0; pp < 8; ++pp) kq |= key_step(pp) == q;
-            if (!kq || M <= 6) {
-              if (q < i) ++slot;
-              ++nslots;
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < 2 * NS; ++u) {
-            if (F0 + (u * (NB - F0)) / (2 * NS) != blk) continue;
-            // this block's chunks, in order; element pairs spread over its slots
-            int first = 0, nch = 0;
-#pragma unroll
-            for (int v = 0; v < 2 * NS; ++v)
-              if (F0 + (v * (NB - F0)) / (2 * NS) == blk) {
-                if (v < u) ++first;
-                ++nch;
-              }
-#pragma unroll
-            for (int e = 0; e < 8; e += 2) {
-              const int item = (first * 4 + e / 2);
-              if ((item * nslots) / (nch * 4) != slot) continue;
-              if (u < NS) {
-                sum_pair(u, e);
-                if (u == 0 && e == 0) atomicAdd(tab + (size_t)DP * TS + pcnt, 1.0);  // count row (h = 1: discard)
-              } else {
-                split_pair(u - NS, e);
-              }
-            }
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-    accs[0] = cn_init(0);
-    accs[1] = cn_init(1);
-    accs[0] = mfma_block(accs[0], 0);
-    __builtin_amdgcn_sched_barrier(0);
-    stamp(0);
-#pragma unroll
-    for (int blk = 1; blk < NB; ++blk) run_block(blk);
-    stamp(1);
-#pragma unroll
-    for (int pp = 0; pp < 8; ++pp) key_pair(accs[(NB - 1) & 1], NB - 1, pp);
-
-    // merge, bound, label, queue (as k_fused)
-    auto pidx = [&](float key, int c) { return ((__float_as_uint(key) & maskq) << 2) | (uint32_t)(4 * h + c); };
-    float k1 = a1[0], k2 = a2[0], k3 = a2[0];
-    uint32_t p1 = pidx(a1[0], 0), p2 = pidx(a2[0], 0);
-    {
-      float m1 = a1[2], m2 = a2[2], m3 = a2[2];
-      uint32_t q1 = pidx(a1[2], 2), q2 = pidx(a2[2], 2);
-      merge3(k1, k2, k3, p1, p2, a1[1], a2[1], a2[1], pidx(a1[1], 1), pidx(a2[1], 1));
-      merge3(m1, m2, m3, q1, q2, a1[3], a2[3], a2[3], pidx(a1[3], 3), pidx(a2[3], 3));
-      merge3(k1, k2, k3, p1, p2, m1, m2, m3, q1, q2);
-    }
-    {
-      uint32_t K1, Q1, K2, Q2, K3, Q3, P1, R1, P2, R2;
-      perm_halves(__float_as_uint(k1), K1, Q1);
-      perm_halves(__float_as_uint(k2), K2, Q2);
-      perm_halves(__float_as_uint(k3), K3, Q3);
-      perm_halves(p1, P1, R1);
-      perm_halves(p2, P2, R2);
-      k1 = __uint_as_float(K1);
-      k2 = __uint_as_float(K2);
-      k3 = __uint_as_float(K3);
-      p1 = P1;
-      p2 = P2;
-      merge3(k1, k2, k3, p1, p2, __uint_as_float(Q1), __uint_as_float(Q2), __uint_as_float(Q3), R1, R2);
-    }
-    const bool same_chain = ((p1 ^ p2) & 7u) == 0u;
-    const float B0 = fmaf(alpha, xn, beta);
-    const float thr2 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k2));
-    const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k3));
-    uint32_t kind = 0;
-    if (!(k2 - k1 > thr2)) kind = (same_chain || !(k3 - k1 > thr3)) ? 2u : 1u;
-    float u1 = 0.0f;
-    KeyBounds kb;
-    const bool refine = REF && __ballot(kind != 0u) != 0ull;
-    if (refine) {
-      kb = key_bounds(xn * s, *A.xabs * s, DP, rho);
-      if (kind != 0u) {
-        u1 = kb.upper(k1);
-        if (u1 < kb.lower(k2))
-          kind = 0u;
-        else if (kind == 2u && !same_chain && kb.lower(k3) > u1)
-          kind = 1u;
-      }
-    }
-    if (__ballot(kind == 2u && same_chain) != 0ull) {
-      const uint32_t cs = p1 & 7u;
-      float o = FLT_MAX;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        uint32_t v0, v1;
-        perm_halves(__float_as_uint(a1[c]), v0, v1);
-        if ((uint32_t)c != cs) o = kmin(o, __uint_as_float(v0));
-        if ((uint32_t)(4 + c) != cs) o = kmin(o, __uint_as_float(v1));
-      }
-      const float thr3x = 2.0f * B0 + rho * (fabsf(k1) + fabsf(o));
-      if (kind == 2u && same_chain && (o - k1 > thr3x || (REF && kb.lower(o) > u1))) kind = 3u;
-    }
-    const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
-    if (h == 0 && valid) A.labels[row] = lab;
-    const bool enq = (h == 0) && valid && (kind != 0);
-    const uint64_t m = __ballot(enq);
-    if (m) {
-      const uint64_t m1 = __ballot(enq && kind == 1);
-      const uint64_t m2 = m & ~m1;
-      const uint64_t below = (1ull << lane) - 1ull;
-      if (enq) {
-        QEntry q;
-        q.row = (uint32_t)row;
-        q.i1 = p1;
-        q.i2 = p2;
-        q.kind = kind;
-        const uint32_t pos = (kind == 1) ? qn + (uint32_t)__popcll(m1 & below)
-                                         : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
-        wq[pos] = q;
-      }
-      qn += (uint32_t)__popcll(m1);
-      qf += (uint32_t)__popcll(m2);
-    }
-    // this tile is summed during the next one's MFMAs (or by the epilogue)
-    prow = row;
-    plab = (valid && kind == 0u) ? lab : KP;
-    pcnt = (valid && kind == 0u && h == 0) ? lab : KP;
-    stamp(2);
-  };
-
-  // prologue: the first tile's rows and split (not overlapped)
-  const int64_t t0 = gw;
-  if (t0 < ntiles) {
-    load_rows(t0, xnext);
-    xnA = load_xn(t0);
-#pragma unroll
-    for (int t = 0; t < NS; ++t) split_chunk(xnext, t, bA[t], lA[t]);
-  }
-  for (int64_t tile = t0; tile < ntiles; tile += 2 * tstride) {
-    tile_step(tile, bA, lA, bB, lB, xnA, xnB);
-    if (tile + tstride >= ntiles) break;
-    tile_step(tile + tstride, bB, lB, bA, lA, xnB, xnA);
-  }
-  // epilogue: the last tile's sums
-  if (t0 < ntiles) {
-    float4 xl[NS][2];
-    const float* xr = A.X + (prow < n ? prow : (n - 1)) * DP + 8 * h;
-#pragma unroll
-    for (int t = 0; t < NS; ++t) {
-      xl[t][0] = *reinterpret_cast<const float4*>(xr + 16 * t);
-      xl[t][1] = *reinterpret_cast<const float4*>(xr + 16 * t + 4);
-    }
-#pragma unroll
-    for (int t = 0; t < NS; ++t) sum_chunk(xl, t, plab);
-    atomicAdd(tab + (size_t)DP * TS + pcnt, 1.0);
-  }
-  if (lane == 0) {
-    A.qcount[2 * gw] = qn;
-    A.qcount[2 * gw + 1] = qf;
-  }
-  if constexpr (STAMP) {
-    if (lane == 0) {
-      for (int i = 0; i < 3; ++i) atomicAdd(&g_stamp[i], st_acc[i]);
-      atomicAdd(&g_stamp[3], __builtin_amdgcn_s_memtime() - st_k0);
-      atomicAdd(&g_stamp[4], __builtin_amdgcn_s_memrealtime() - st_r0);
-      atomicAdd(&g_stamp[5], 1ull);
-    }
-  }
-  __syncthreads();
-  const int d1 = A.d + 1;
-  for (int i = threadIdx.x; i < (DP + 1) * KP; i += WAVES * 64) {
-    const int j = i / (DP + 1);
-    const int f = i - j * (DP + 1);
-    const double v = tab[(size_t)f * TS + j];
-    if (v != 0.0 && (f < A.d || f == DP) && j < A.k) atomicAdd(A.stats + (size_t)j * d1 + (f == DP ? A.d : f), v);
-  }
-}
-#endif  // KM_DIAG (k_fusedp)
-
-#ifdef KM_DIAG  // the fast screen is a diagnostic-build experiment (DESIGN.md "Fast screen")
-// ---------------------------------------------------------------------------
-// Fast screen (k_fused1): ONE fp16 image of -2cs (128 AGPRs instead of 256)
-// against the row as one fp16 part (NX = 1: one MFMA per product instead of
-// three) or hi + lo (NX = 2), with a PAIRWISE error bound (DESIGN.md §2 "Fast
-// screen").  The image is rounded per feature to either fp16 neighbour of
-// a = -2 c' (c' = c32 s), chosen so that alpha . c' ~ 0 (alpha = image - a).
-// For a point X (scaled row) and centroids j, i, the screen errors satisfy
-//   |E_j - E_i| <= C0 + c (D_j + D_i),   D_j = ||X - c'_j||,
-//   c  = 2 ||beta|| + max ||alpha||            (beta: row rounding, <= u16 ||X||)
-//   C0 = 2 Acc + 2 nu + 4 u24 cm xn + 2 max |alpha . c'| + 2 max||alpha|| ||beta||
-// since  E_j = acc_j + nu_j - 2 gamma_j.X - 2 c'_j.beta + alpha_j.X + alpha_j.beta
-// with alpha_j.X = alpha_j.c'_j + alpha_j.(X - c'_j): the errors that matter
-// for a decision scale with the DISTANCES to the two centroids, not with
-// ||c|| ||x|| as in a global bound.  D_j is bounded from the key itself.
-// ---------------------------------------------------------------------------
-
-// one fp16 step from h towards +inf (up) or -inf
-__device__ __forceinline__ _Float16 f16_step(_Float16 h, bool up) {
-  uint16_t b = __builtin_bit_cast(uint16_t, h);
-  if ((b & 0x7fffu) == 0u) return __builtin_bit_cast(_Float16, (uint16_t)(up ? 0x0001u : 0x8001u));
-  const bool neg = (b & 0x8000u) != 0u;
-  b = (up != neg) ? (uint16_t)(b + 1u) : (uint16_t)(b - 1u);
-  return __builtin_bit_cast(_Float16, b);
-}
-
-// Balanced image, written fragment-linear (piece (b, t), lane l, 8 halves:
-// the k_frag_images layout), one thread per centroid: a greedy pass over the
-// features picks the neighbour that keeps the running alpha . c' smallest,
-// then two passes of single flips that shrink it.  bal[0] = max_j ||alpha_j||,
-// bal[1] = max_j |alpha_j . c'_j| (scaled units, rounded up; real centroids).
-__global__ __launch_bounds__(512) void k_prep_bal(const float* __restrict__ C32, int k, int kp, int dp,
-                                                  const float* __restrict__ xabs, const float* __restrict__ cabs,
-                                                  const float* __restrict__ cmaxp, int nx,
-                                                  uint16_t* __restrict__ imgF, float* __restrict__ bal,
-                                                  const int* __restrict__ gate) {
-  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
-  __shared__ float red[2][8];
-  const float s = mfma_scale(*xabs, *cabs);
-  const int ns = dp / 16;
-  float an = 0.0f, ac = 0.0f;
-  for (int j = threadIdx.x; j < kp; j += blockDim.x) {
-    const float* cr = C32 + (size_t)j * dp;
-    auto at = [&](int f) -> uint16_t& {
-      const int b = j >> 5, t = f >> 4, l = (j & 31) + 32 * ((f >> 3) & 1);
-      return imgF[((size_t)((b * ns + t) * 64 + l)) * 8 + (f & 7)];
-    };
-    // alpha_f c'_f for image value v (exact in float64: both factors <= 24 bits)
-    auto err = [&](_Float16 v, float a) { return ((double)(float)v - (double)a) * (-0.5 * (double)a); };
-    double run = 0.0;
-    for (int f = 0; f < dp; ++f) {
-      const float a = -2.0f * cr[f] * s;
-      const _Float16 h = (_Float16)a;
-      const _Float16 o = ((float)h == a) ? h : f16_step(h, a > (float)h);
-      const double eh = err(h, a), eo = err(o, a);
-      const bool po = fabs(run + eo) < fabs(run + eh);
-      run += po ? eo : eh;
-      at(f) = __builtin_bit_cast(uint16_t, po ? o : h);
-    }
-    for (int pass = 0; pass < 2; ++pass)
-      for (int f = 0; f < dp; ++f) {
-        const float a = -2.0f * cr[f] * s;
-        const _Float16 h = (_Float16)a;
-        const _Float16 o = ((float)h == a) ? h : f16_step(h, a > (float)h);
-        const _Float16 cur = __builtin_bit_cast(_Float16, at(f));
-        const _Float16 alt = (__builtin_bit_cast(uint16_t, cur) == __builtin_bit_cast(uint16_t, h)) ? o : h;
-        const double ec = err(cur, a), ea = err(alt, a);
-        if (fabs(run - ec + ea) < fabs(run)) {
-          run = run - ec + ea;
-          at(f) = __builtin_bit_cast(uint16_t, alt);
-        }
-      }
-    // exact recount of both maxima from the stored image
-    double nn = 0.0, sum = 0.0, sabs = 0.0;
-    for (int f = 0; f < dp; ++f) {
-      const float a = -2.0f * cr[f] * s;
-      const _Float16 v = __builtin_bit_cast(_Float16, at(f));
-      const double al = (double)(float)v - (double)a;
-      nn += al * al;
-      const double e = err(v, a);
-      sum += e;
-      sabs += fabs(e);
-    }
-    if (j < k) {
-      const double nb = sqrt(nn) * (1.0 + 1e-12);
-      const double cb = fabs(sum) + (double)dp * 2.3e-16 * sabs;  // float64 summation slack
-      an = fmaxf(an, (float)nb * (1.0f + 2.0f * U24));
-      ac = fmaxf(ac, (float)cb * (1.0f + 2.0f * U24) + 1e-30f);
-    }
-  }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    an = fmaxf(an, __shfl_xor(an, o));
-    ac = fmaxf(ac, __shfl_xor(ac, o));
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-    red[0][wave] = an;
-    red[1][wave] = ac;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float m0 = 0.0f, m1 = 0.0f;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
-      m0 = fmaxf(m0, red[0][w]);
-      m1 = fmaxf(m1, red[1][w]);
-    }
-    // pairwise-bound constants (scaled units), every per-point term affine
-    // in xn = s ||x|| (per-row upper bound): bal[2..10] = s, cm, G1, G0, c1,
-    // c0, h1, h0, rho2 (k_fused1 reads them as scalars)
-    const float cm = *cmaxp * s;
-    const float pm = (*cabs * s) * (*xabs * s) * 1.0001f;
-    const float sq = sqrtf((float)dp);
-    // fp16 subnormals (flushed or not): 2^-14 per element, on row and image
-    // (|alpha_f| grows by <= 2^-14 only where |c'_f| < 2^-15)
-    const float an = m0 + 6.103515625e-05f * sq, ac = m1 + (float)dp * 1.862645149230957e-09f;
-    const float NM = (float)(nx * dp / 16);  // MFMAs per score chain
-    // ||beta|| <= bq1 xn + bq0 (row rounding: u16 = 2^-11; hi + lo: u16^2)
-    const float bq1 = (nx == 1 ? 4.8828125e-4f : 2.384185791015625e-07f) * 1.0001f;
-    const float bq0 = 6.103515625e-05f * sq;
-    // accumulation (one rounding of |D| <= cm^2 + 2 cm xn per MFMA, and the
-    // in-group alignment truncation, 14 u24 x the largest product 2 pm)
-    const float acc1 = NM * U24 * 2.01f * cm;
-    const float acc0 = NM * U24 * (cm * cm + 28.1f * pm);
-    const float nu = 1.01f * U24 * cm * cm;  // ||c||^2 s^2 rounding
-    // |E_j| <= G = Acc + nu + 2 u24 cm xn + 2 cm ||beta|| + max||alpha|| (xn + ||beta||)
-    bal[2] = s;
-    bal[3] = cm;
-    bal[4] = acc1 + 2.01f * U24 * cm + 2.01f * cm * bq1 + an * (1.0f + bq1);
-    bal[5] = acc0 + nu + 2.01f * cm * bq0 + an * bq0;
-    bal[6] = 2.0f * bq1;
-    bal[7] = 2.0f * bq0 + an * 1.0001f;
-    bal[8] = 2.0f * acc1 + 4.01f * U24 * cm + 2.0f * an * bq1;
-    bal[9] = 2.0f * acc0 + 2.0f * nu + 2.0f * ac + 2.0f * an * bq0;
-    // key truncation (index bits of kp) plus the rounding of a key difference
-    bal[10] = __builtin_ldexpf(1.0f, ceil_log2(kp) - 2 - 23) * 1.01f + 2.0f * U24;
-  }
-}
-
-// NX = 1: the row as one fp16 part; NX = 2: hi + lo (the image stays one part).
-// bal = {max ||alpha||, max |alpha . c'|} from k_prep_bal; cmaxp = max ||c|| (unscaled)
-template <int NS, int NB, int NX, bool STATS, int WAVES>
-__global__ __launch_bounds__(WAVES * 64, 1) void k_fused1(FusedArgs A, const float* __restrict__ bal,
-                                                          const float* __restrict__ cmaxp) {
-  if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
-  constexpr int DP = 16 * NS;
-  constexpr int KP = 32 * NB;
-  constexpr int B = ceil_log2_c(KP);
-  static_assert(B >= 3 && B - 2 <= 12, "index bits");
-  static_assert(NB >= 2, "pipelined blocks");
-  static_assert(NX == 1 || NX == 2, "row parts");
-  constexpr uint32_t maskq = (1u << (B - 2)) - 1u;
-  constexpr int TS = KP;  // sum table row stride (KP + 2, which moves the lane halves to opposite bank halves: no gain)
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* sCn = reinterpret_cast<float*>(smem);                  // ||c||^2 s^2 [KP]
-  double* tab = reinterpret_cast<double*>(smem + KP * 4);        // [DP + 1][TS]
-
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int r = lane & 31;
-  const int h = lane >> 5;
-  for (int i = threadIdx.x; i < KP; i += WAVES * 64) sCn[i] = A.cn2s[i];
-  if constexpr (STATS)
-    for (int i = threadIdx.x; i < (DP + 1) * TS; i += WAVES * 64) tab[i] = 0.0;
-  f16x8 Ahi[NB][NS];
-#pragma unroll
-  for (int b = 0; b < NB; ++b)
-#pragma unroll
-    for (int t = 0; t < NS; ++t) Ahi[b][t] = __builtin_bit_cast(f16x8, A.ChiF[(b * NS + t) * 64 + lane]);
-#pragma unroll
-  for (int b = 0; b < NB; ++b)
-#pragma unroll
-    for (int t = 0; t < NS; ++t) asm volatile("" : "+a"(Ahi[b][t]));
-  __syncthreads();
-
-  // pairwise-bound constants from k_prep_bal (uniform: scalar loads)
-  const float s = bal[2], cm = bal[3];
-  const float G1 = bal[4], G0 = bal[5], c1 = bal[6], c0 = bal[7], h1 = bal[8], h0 = bal[9];
-  const float rho2 = bal[10];
-
-  const int64_t n = A.n;
-  const int64_t ntiles = (n + 31) / 32;
-  const uint32_t gw = blockIdx.x * WAVES + wave;
-  QEntry* wq = A.queue + (size_t)gw * A.seg;
-  uint32_t qn = 0, qf = 0;
-  const int64_t tstride = (int64_t)gridDim.x * WAVES;
-  const float4* cnl = reinterpret_cast<const float4*>(sCn + 4 * h);  // + 8 blk + 2 g4
-
-  auto load_tile = [&](int64_t tile, float4 (&xq)[NS][2], float& xnq) {
-    const int64_t row = tile * 32 + r;
-    const int64_t rr = row < n ? row : (n - 1);
-    const float* xr = A.X + rr * DP + 8 * h;
-#pragma unroll
-    for (int t = 0; t < NS; ++t) {
-      xq[t][0] = *reinterpret_cast<const float4*>(xr + 16 * t);
-      xq[t][1] = *reinterpret_cast<const float4*>(xr + 16 * t + 4);
-    }
-    xnq = A.xnorm[rr];
-  };
-
-  auto process_tile = [&](int64_t tile, const float4 (&xc)[NS][2], float xn) {
-    const int64_t row = tile * 32 + r;
-    const bool valid = row < n;
-    // B operand: lane (r, h) holds features [16t + 8h, +8) of point r
-    f16x8 bh[NS], bl[NS];
-#pragma unroll
-    for (int t = 0; t < NS; ++t) {
-      const float xv[8] = {xc[t][0].x, xc[t][0].y, xc[t][0].z, xc[t][0].w,
-                           xc[t][1].x, xc[t][1].y, xc[t][1].z, xc[t][1].w};
-#pragma unroll
-      for (int e = 0; e < 8; e += 2) {
-        const float xs0 = xv[e] * s, xs1 = xv[e + 1] * s;
-        const f16x2 hp = {(_Float16)xs0, (_Float16)xs1};
-        bh[t][e] = hp[0];
-        bh[t][e + 1] = hp[1];
-        if constexpr (NX == 2) {
-          const f16x2 lo = split_lo(hp, xs0, xs1);
-          bl[t][e] = lo[0];
-          bl[t][e + 1] = lo[1];
-        }
-      }
-    }
-    float a1[4], a2[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) a1[c] = a2[c] = FLT_MAX;
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int t = 0; t < NS; ++t) asm volatile("" : "+a"(Ahi[b][t]));
-    auto cn_init = [&](int blk) {
-      f32x16 acc;
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const float4 cv = cnl[8 * blk + 2 * g4];
-        acc[4 * g4 + 0] = cv.x;
-        acc[4 * g4 + 1] = cv.y;
-        acc[4 * g4 + 2] = cv.z;
-        acc[4 * g4 + 3] = cv.w;
-      }
-      return acc;
-    };
-    auto mfma_block = [&](f32x16 acc, int blk) {
-#pragma unroll
-      for (int t = 0; t < NS; ++t) {
-        if constexpr (NX == 2) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bl[t], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bh[t], acc, 0, 0, 0);
-      }
-      return acc;
-    };
-    // register reg holds centroid j = 32 blk + 4h + (reg & 3) + 8 (reg >> 2);
-    // chain reg & 3 keeps the top two keys (score | j >> 2) (as in k_fused)
-    auto keys_block = [&](const f32x16& acc, int blk) {
-      const uint32_t jq = (uint32_t)(8 * blk + h);
-#pragma unroll
-      for (int q = 0; q < 16; q += 8)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int ra = q + c, rb = q + c + 4;
-          const float ka = __uint_as_float((__float_as_uint(acc[ra]) & ~maskq) | (jq | (uint32_t)(2 * (ra >> 2))));
-          const float kb = __uint_as_float((__float_as_uint(acc[rb]) & ~maskq) | (jq | (uint32_t)(2 * (rb >> 2))));
-          const float t = __builtin_amdgcn_fmed3f(a1[c], ka, kb);
-          a1[c] = __builtin_fminf(__builtin_fminf(a1[c], ka), kb);
-          a2[c] = __builtin_fminf(a2[c], t);
-        }
-    };
-    constexpr int NMB = NX * NS;  // MFMAs per block
-    f32x16 accs[2];
-    f32x16 cinit = cn_init(1);
-    accs[0] = mfma_block(cn_init(0), 0);
-#pragma unroll
-    for (int blk = 1; blk < NB; ++blk) {
-      const f32x16 cin = cinit;
-      if (blk + 1 < NB) cinit = cn_init(blk + 1);
-      accs[blk & 1] = mfma_block(cin, blk);
-      keys_block(accs[(blk - 1) & 1], blk - 1);
-      // MFMA, next block's init reads, then (VALU x m, MFMA) pairs
-      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-      for (int i = 0; i < NMB - 1; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x2, 40 / NMB + 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    keys_block(accs[(NB - 1) & 1], NB - 1);
-
-    auto pidx = [&](float key, int c) { return ((__float_as_uint(key) & maskq) << 2) | (uint32_t)c; };
-    float k1 = a1[0], k2 = a2[0], k3 = a2[0];
-    uint32_t p1 = pidx(a1[0], 0), p2 = pidx(a2[0], 0);
-    {
-      float m1 = a1[2], m2 = a2[2], m3 = a2[2];
-      uint32_t q1 = pidx(a1[2], 2), q2 = pidx(a2[2], 2);
-      merge3(k1, k2, k3, p1, p2, a1[1], a2[1], a2[1], pidx(a1[1], 1), pidx(a2[1], 1));
-      merge3(m1, m2, m3, q1, q2, a1[3], a2[3], a2[3], pidx(a1[3], 3), pidx(a2[3], 3));
-      merge3(k1, k2, k3, p1, p2, m1, m2, m3, q1, q2);
-    }
-    {
-      uint32_t K1, Q1, K2, Q2, K3, Q3, P1, R1, P2, R2;
-      perm_halves(__float_as_uint(k1), K1, Q1);
-      perm_halves(__float_as_uint(k2), K2, Q2);
-      perm_halves(__float_as_uint(k3), K3, Q3);
-      perm_halves(p1, P1, R1);
-      perm_halves(p2, P2, R2);
-      k1 = __uint_as_float(K1);
-      k2 = __uint_as_float(K2);
-      k3 = __uint_as_float(K3);
-      p1 = P1;
-      p2 = P2;
-      merge3(k1, k2, k3, p1, p2, __uint_as_float(Q1), __uint_as_float(Q2), __uint_as_float(Q3), R1, R2);
-    }
-    const bool same_chain = ((p1 ^ p2) & 7u) == 0u;
-    // pairwise test of the best against every key >= kj
-    const float xs = xn * s;
-    const float G = fmaf(G1, xs, G0), cs = fmaf(c1, xs, c0), C0 = fmaf(h1, xs, h0);
-    const float x2 = xs * xs;
-    const float mono = 1.01f * cs + U24 * cm;
-    // D(K): upper bound of ||X - c'_j|| for a centroid with key K
-    auto Dof = [&](float K) {
-      const float Kp = K + rho2 * fabsf(K);
-      const float arg = Kp + G + x2 + 4.0f * U24 * (fabsf(Kp) + G + x2);
-      return sqrtf(fmaxf(arg, 0.0f)) * (1.0f + 4.0f * U24) + U24 * cm;
-    };
-    const float D1 = Dof(k1);
-    // every centroid with key >= kj is provably farther than the best: the
-    // gap beats the pair bound at kj, and the gap grows faster than the bound
-    // beyond kj (d/dK of c D(K) < 1/2 once D >= 1.01 c)
-    auto sep = [&](float kj) {
-      const float Dj = Dof(kj);
-      const float gap = (kj - k1) - rho2 * (fabsf(k1) + fabsf(kj));
-      const float P = fmaf(cs, D1 + Dj, C0) * 1.0002f;
-      return gap > P && Dj >= mono;
-    };
-    uint32_t kind = 0;
-    if (!sep(k2)) kind = (same_chain || !sep(k3)) ? 2u : 1u;
-    // p1, p2 in one chain but every other chain's best separated: scan only
-    // that chain (kind 3), as in k_fused
-    if (__ballot(kind == 2u && same_chain) != 0ull) {
-      const uint32_t cs8 = p1 & 7u;
-      float o = FLT_MAX;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        uint32_t v0, v1;
-        perm_halves(__float_as_uint(a1[c]), v0, v1);
-        if ((uint32_t)c != cs8) o = kmin(o, __uint_as_float(v0));
-        if ((uint32_t)(4 + c) != cs8) o = kmin(o, __uint_as_float(v1));
-      }
-      if (kind == 2u && same_chain && sep(o)) kind = 3u;
-    }
-    const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
-    if (h == 0 && valid) A.labels[row] = lab;
-    const bool enq = (h == 0) && valid && (kind != 0);
-    const uint64_t m = __ballot(enq);
-    if (m) {
-      const uint64_t m1 = __ballot(enq && kind == 1);
-      const uint64_t m2 = m & ~m1;
-      const uint64_t below = (1ull << lane) - 1ull;
-      if (enq) {
-        QEntry q;
-        q.row = (uint32_t)row;
-        q.i1 = p1;
-        q.i2 = p2;
-        q.kind = kind;
-        const uint32_t pos = (kind == 1) ? qn + (uint32_t)__popcll(m1 & below)
-                                         : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
-        wq[pos] = q;
-      }
-      qn += (uint32_t)__popcll(m1);
-      qf += (uint32_t)__popcll(m2);
-    }
-    if constexpr (STATS) {
-      if (valid && kind == 0) {
-        double* tp = tab + (size_t)(8 * h) * TS + lab;
-#pragma unroll
-        for (int t = 0; t < NS; ++t) {
-          const float4 v0 = xc[t][0], v1 = xc[t][1];
-          const float xe[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-          for (int e = 0; e < 8; ++e) atomicAdd(tp + (size_t)(16 * t + e) * TS, (double)xe[e]);
-        }
-        if (h == 0) atomicAdd(tab + (size_t)DP * TS + lab, 1.0);  // count row
-      }
-    }
-  };
-
-  {
-    float4 xb0[NS][2], xb1[NS][2];
-    float xn0 = 0.0f, xn1 = 0.0f;
-    load_tile(gw, xb0, xn0);
-    for (int64_t tile = gw; tile < ntiles; tile += 2 * tstride) {
-      const int64_t t1 = tile + tstride;
-      load_tile(t1, xb1, xn1);
-      process_tile(tile, xb0, xn0);
-      if (t1 >= ntiles) break;
-      load_tile(t1 + tstride, xb0, xn0);
-      process_tile(t1, xb1, xn1);
-    }
-  }
-  if (lane == 0) {
-    A.qcount[2 * gw] = qn;
-    A.qcount[2 * gw + 1] = qf;
-  }
-  if constexpr (STATS) {
-    __syncthreads();
-    const int d1 = A.d + 1;
-    for (int i = threadIdx.x; i < (DP + 1) * KP; i += WAVES * 64) {
-      const int j = i / (DP + 1);
-      const int f = i - j * (DP + 1);
-      const double v = tab[(size_t)f * TS + j];
-      if (v != 0.0 && (f < A.d || f == DP) && j < A.k) atomicAdd(A.stats + (size_t)j * d1 + (f == DP ? A.d : f), v);
-    }
-  }
-}
-
-#endif  // KM_DIAG
+#include "km_diag.inc"
+#endif
 
 // fragment-linear copies of the hi / lo images: piece (b, t), lane l holds
 // 8 halves of row 32 b + (l & 31), features 16 t + 8 (l >> 5) .. + 8
