@@ -27,6 +27,7 @@
 namespace km {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 static constexpr float U24 = 5.9604644775390625e-08f;  // 2^-24, fp32 unit roundoff
 
@@ -49,6 +50,29 @@ __device__ __forceinline__ void top3_insert(float& k1, float& k2, float& k3, flo
 
 __device__ __forceinline__ float key_of(float score, uint32_t idx, uint32_t mask) {
   return __uint_as_float((__float_as_uint(score) & ~mask) | idx);
+}
+
+// Cross-lane exchanges of the 16x16 MFMA layouts (lane l: column l & 15,
+// quarter l >> 4).  perm_quarters: lo = value of lane (l & ~16), hi = value of
+// lane (l | 16).  swap_halves(v0, v1): lanes 0-31 get v0 of lanes l and
+// l + 32, lanes 32-63 get v1 of lanes l - 32 and l (the lower lane's first):
+// v_permlane32_swap exchanges the upper half of its first operand with the
+// lower half of its second.
+__device__ __forceinline__ void perm_halves(uint32_t v, uint32_t& lo, uint32_t& hi) {
+  // lo = value of lane (l & 31), hi = value of lane (l | 32), in every lane
+  const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  lo = p[0];
+  hi = p[1];
+}
+__device__ __forceinline__ void perm_quarters(uint32_t v, uint32_t& lo, uint32_t& hi) {
+  const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  lo = p[0];
+  hi = p[1];
+}
+__device__ __forceinline__ void swap_halves(uint32_t v0, uint32_t v1, uint32_t& lo, uint32_t& hi) {
+  const auto p = __builtin_amdgcn_permlane32_swap(v0, v1, false, false);
+  lo = p[0];
+  hi = p[1];
 }
 
 __device__ inline double wave_sum(double v) {
@@ -104,8 +128,8 @@ __host__ __device__ inline float screen_icpt(float cm_s, float pm_s, int dp, int
   return 1.5f * (U24 * cm_s * cm_s + ce.nr * U24 * cm_s * cm_s + ce.nt * 28.0f * U24 * pm_s +
                  2.0f * U24 * sqrtf((float)dp) * cm_s);
 }
-__host__ __device__ inline float screen_b0(float xn_s, float cm_s, float pm_s, int dp) {
-  return fmaf(screen_slope(cm_s, dp), xn_s, screen_icpt(cm_s, pm_s, dp));
+__host__ __device__ inline float screen_b0(float xn_s, float cm_s, float pm_s, int dp, int shape16 = 0) {
+  return fmaf(screen_slope(cm_s, dp, shape16), xn_s, screen_icpt(cm_s, pm_s, dp, shape16));
 }
 
 // Per-key screening bounds (scaled units), used where the global-cmax test
@@ -874,6 +898,26 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
         acc[t] += (float)f.hi[0] + (float)f.lo[1] + (float)bl[t][2] + (float)bh[t][3];
         return acc;
       }
+      if constexpr (ABL == 4) {
+        // diagnostic (results wrong): the same MACs on v_mfma_f32_16x16x32_f16
+        // (two per 32x32x16, the same operand registers, four 4-register
+        // accumulators in the 16 of acc) -- the shape's clock lever in this
+        // kernel, with no key updates (compare ABL = 1)
+        f32x4 q[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = f32x4{acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]};
+        q[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.hi, bl[t], q[0], 0, 0, 0);
+        q[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.hi, bl[t], q[1], 0, 0, 0);
+        q[2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.lo, bh[t], q[2], 0, 0, 0);
+        q[3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.lo, bh[t], q[3], 0, 0, 0);
+        q[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.hi, bh[t], q[0], 0, 0, 0);
+        q[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.hi, bh[t], q[1], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) acc[4 * i + e2] = q[i][e2];
+        return acc;
+      }
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.hi, bl[t], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.lo, bh[t], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.hi, bh[t], acc, 0, 0, 0);
@@ -890,7 +934,7 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
       }
     };
     auto key_update = [&](const f32x16& acc, int reg) {
-      if constexpr (ABL == 1) {
+      if constexpr (ABL == 1 || ABL == 4) {
         if (reg == 0) a1[0] = fminf(a1[0], acc[0] + acc[15]);
         asm volatile("" ::"v"(acc[reg]));
         return;
@@ -1148,6 +1192,466 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
 // Keys, chains, the rigorous bound and the queue are those of k_assign_mfma
 // (top-3 chains).  X is read once per centroid chunk (once for k <= 256).
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// k_assign_mfma16: k_assign_mfma on v_mfma_f32_16x16x32_f16 (dp a multiple of
+// 32).  Same chunked LDS images, LDS-DMA and queue / candidate-list logic, the
+// same 32 rows per wave; a block of 32 centroids is two 16-centroid halves
+// (cb) x two 16-row groups (pg), and an image piece (blk, cb NS/2 + sl) holds,
+// lane l, the 8 halves of centroid 32 blk + 16 cb + (l & 15), features
+// 32 sl + 8 (l >> 4).  On the MFMA-only ablation at c5 (12 waves) the shape
+// runs 2.12 vs 1.92 GHz at equal MFMA busy: 109 vs 121 ms (DESIGN.md
+// section 4).  Chains are (j & 3, quarter q = l >> 4) per row group: 16 per
+// row; after the chunks the row groups are reduce-scattered over the lane
+// halves and merged over quarter pairs (as k_fused16), so lanes l and l ^ 16
+// own row (l & 15) + 16 (l >> 5).  The bound is screen_b0's 16x16x32 model.
+// ---------------------------------------------------------------------------
+template <int NS, int WAVES, bool T2 = false>
+__global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_assign_mfma16(MfmaArgs A) {
+  if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
+  static_assert(NS % 2 == 0, "dp a multiple of 32");
+  constexpr int DP = 16 * NS;
+  constexpr int NS2 = NS / 2;      // 32-feature slabs
+  constexpr int BLKB = NS * 1024;  // bytes of one block's fragments (one of hi / lo)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int KC = A.KC;
+  const size_t himg = (size_t)(KC / 32) * BLKB;
+  const size_t bufsz = ((2 * himg + (size_t)KC * 4) + 15) / 16 * 16;
+  char* sHi = smem;
+  char* sLo = smem + himg;
+  float* sCn = reinterpret_cast<float*>(smem + 2 * himg);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int c16 = lane & 15;
+  const int q = lane >> 4;
+  const int pgo = lane >> 5;           // the row group this lane owns after the merge
+  const int prow = c16 + 16 * pgo;     // its row within the tile
+  const int kp = A.kp;
+  const int64_t n = A.n;
+  const int b = ceil_log2(kp);  // kp is a multiple of 64: b >= 6
+  const uint32_t maskq = (1u << (b - 2)) - 1u;
+  const float s = mfma_scale(*A.xabs, *A.cabs);
+  const float cm = *A.cmax * s;
+  const float pm = (*A.cabs * s) * (*A.xabs * s) * 1.0001f;
+  const float rho = __builtin_ldexpf(1.0f, b - 2 - 23) * 1.01f;  // key truncation (relative)
+  const int nchunks = (kp + KC - 1) / KC;
+  const int64_t ntiles = (n + 31) / 32;
+  const int64_t nwt = (ntiles + WAVES - 1) / WAVES;
+
+  // piece pc = blk NS + tt of a chunk, tt = cb NS2 + sl: lane l's 16 bytes
+  auto piece_src = [&](int pc, int l) {
+    const int blk = pc / NS, tt = pc - blk * NS;
+    const int cb = tt / NS2, sl = tt - cb * NS2;
+    return ((size_t)(blk * 32 + 16 * cb + (l & 15)) * DP + 32 * sl + 8 * (l >> 4)) * 2;
+  };
+  auto stage = [&](int ch) {
+    const int kc = min(KC, kp - ch * KC);
+    const int npieces = (kc / 32) * NS * 64;
+    const char* gh = reinterpret_cast<const char*>(A.Chi + (size_t)ch * KC * DP);
+    const char* gl = reinterpret_cast<const char*>(A.Clo + (size_t)ch * KC * DP);
+    for (int id = threadIdx.x; id < npieces; id += WAVES * 64) {
+      const size_t src = piece_src(id >> 6, id & 63);
+      *reinterpret_cast<uint4*>(sHi + (size_t)id * 16) = *reinterpret_cast<const uint4*>(gh + src);
+      *reinterpret_cast<uint4*>(sLo + (size_t)id * 16) = *reinterpret_cast<const uint4*>(gl + src);
+    }
+    for (int id = threadIdx.x; id < kc; id += WAVES * 64) sCn[id] = A.cn2s[(size_t)ch * KC + id];
+  };
+  auto stage_async = [&](int ch, int bf) {
+    const int kc = min(KC, kp - ch * KC);
+    const int npc = (kc / 32) * NS;
+    char* dHi = smem + (size_t)bf * bufsz;
+    char* dLo = dHi + himg;
+    char* dCn = dHi + 2 * himg;
+    const char* gh = reinterpret_cast<const char*>(A.Chi + (size_t)ch * KC * DP);
+    const char* gl = reinterpret_cast<const char*>(A.Clo + (size_t)ch * KC * DP);
+    for (int pc = wave; pc < npc; pc += WAVES) {
+      const size_t src = piece_src(pc, lane);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(gh + src),
+                                       (__attribute__((address_space(3))) void*)(dHi + (size_t)pc * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(gl + src),
+                                       (__attribute__((address_space(3))) void*)(dLo + (size_t)pc * 1024), 16, 0, 0);
+    }
+    const char* gc = reinterpret_cast<const char*>(A.cn2s + (size_t)ch * KC);
+    for (int pc = wave; pc * 1024 < kc * 4; pc += WAVES)
+      if (pc * 1024 + lane * 16 < kc * 4)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(gc + pc * 1024 + lane * 16),
+                                         (__attribute__((address_space(3))) void*)(dCn + pc * 1024), 16, 0, 0);
+  };
+
+  int cbuf = 0;
+  if (nchunks == 1) {
+    stage(0);
+    __syncthreads();
+  } else if ((int64_t)blockIdx.x < nwt) {
+    stage_async(0, 0);
+  }
+
+  const uint32_t gw = blockIdx.x * WAVES + wave;
+  QEntry* wq = A.queue + (size_t)gw * A.seg;
+  uint32_t qn = 0, qf = 0;
+  const char* laneHi = sHi + lane * 16;
+  const char* laneLo = sLo + lane * 16;
+  const float* laneCn = sCn + 4 * q;
+  auto point_at = [&](int bf) {
+    laneHi = smem + (size_t)bf * bufsz + lane * 16;
+    laneLo = laneHi + himg;
+    laneCn = reinterpret_cast<const float*>(smem + (size_t)bf * bufsz + 2 * himg) + 4 * q;
+  };
+
+  for (int64_t wt = blockIdx.x; wt < nwt; wt += gridDim.x) {
+    const int64_t tile = wt * WAVES + wave;
+    if (nchunks == 1 && tile >= ntiles) break;  // no barriers below in this mode
+    const int64_t row = tile * 32 + prow;       // the row this lane owns after the merge
+    const bool valid = row < n;
+
+    // B operands: lane l holds features 32 sl + 8 q .. + 8 of rows 16 pg + (l & 15)
+    f16x8 bh[2][NS2], bl[2][NS2];
+    float xx[2] = {0.0f, 0.0f};
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg) {
+      const int64_t rg = tile * 32 + 16 * pg + c16;
+      const float* xr = A.X + (rg < n ? rg : (n - 1)) * DP + 8 * q;
+#pragma unroll
+      for (int sl = 0; sl < NS2; ++sl) {
+        const float4 v0 = *reinterpret_cast<const float4*>(xr + 32 * sl);
+        const float4 v1 = *reinterpret_cast<const float4*>(xr + 32 * sl + 4);
+        const float xv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xs = xv[e] * s;
+          const _Float16 hi = (_Float16)xs;
+          bh[pg][sl][e] = hi;
+          bl[pg][sl][e] = (_Float16)(xs - (float)hi);
+          xx[pg] = fmaf(xs, xs, xx[pg]);
+        }
+      }
+    }
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg) {  // the four quarters hold disjoint features of a row
+      xx[pg] += __shfl_xor(xx[pg], 16);
+      xx[pg] += __shfl_xor(xx[pg], 32);
+    }
+
+    float a1[2][4], a2[2][4], a3[2][4];
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) a1[pg][c] = a2[pg][c] = a3[pg][c] = FLT_MAX;
+
+    struct Acc {
+      f32x4 v[2][2];  // [cb][pg]
+    };
+    auto init_acc = [&](int blk) {
+      Acc a;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const float4 cv = *reinterpret_cast<const float4*>(laneCn + blk * 32 + 16 * cb);
+        const f32x4 c4 = {cv.x, cv.y, cv.z, cv.w};
+        a.v[cb][0] = c4;
+        a.v[cb][1] = c4;
+      }
+      return a;
+    };
+    struct Frag {
+      f16x8 hi, lo;
+    };
+    auto load_frag = [&](int blk, int tt) {
+      const size_t off = (size_t)blk * BLKB + (size_t)tt * 1024;
+      Frag f;
+      f.hi = *reinterpret_cast<const f16x8*>(laneHi + off);
+      f.lo = *reinterpret_cast<const f16x8*>(laneLo + off);
+      return f;
+    };
+    // piece tt = cb NS2 + sl: the half cb's contribution of slab sl, both row groups
+    auto mfma_step = [&](Acc& a, const Frag& f, int tt) {
+      const int cb = tt / NS2, sl = tt - (tt / NS2) * NS2;
+#pragma unroll
+      for (int pg = 0; pg < 2; ++pg)
+        a.v[cb][pg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.hi, bl[pg][sl], a.v[cb][pg], 0, 0, 0);
+#pragma unroll
+      for (int pg = 0; pg < 2; ++pg)
+        a.v[cb][pg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.lo, bh[pg][sl], a.v[cb][pg], 0, 0, 0);
+#pragma unroll
+      for (int pg = 0; pg < 2; ++pg)
+        a.v[cb][pg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.hi, bh[pg][sl], a.v[cb][pg], 0, 0, 0);
+    };
+    // register i of accumulator (cb, pg): centroid j = 32 blk + 16 cb + 4 q + i;
+    // chain (i, q) of row group pg stores j >> 2 = 8 blk + 4 cb + q in the key
+    uint32_t jg[2];
+    auto set_jg = [&](uint32_t jq) {  // jq = j >> 2 of the block's cb = 0, q = 0 (+ q added)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        jg[cb] = jq + 4u * (uint32_t)cb + (uint32_t)q;
+        asm volatile("" : "+v"(jg[cb]));  // keep it a register: one v_and_or per key
+      }
+    };
+    auto key_of2 = [&](float v, int cb) { return __uint_as_float((__float_as_uint(v) & ~maskq) | jg[cb]); };
+    // update u of the block's 16 (T2: 8 pairs): pg = u >> 3, c = u & 3 (T2: u = 4 pg + c)
+    auto key_update = [&](const Acc& a, int u) {
+      const int pg = u >> 3, cb = (u >> 2) & 1, c = u & 3;
+      top3_insert(a1[pg][c], a2[pg][c], a3[pg][c], key_of2(a.v[cb][pg][c], cb));
+    };
+    auto key_pair = [&](const Acc& a, int u) {
+      const int pg = u >> 2, c = u & 3;
+      const float ka = key_of2(a.v[0][pg][c], 0);
+      const float kb = key_of2(a.v[1][pg][c], 1);
+      const float tm = __builtin_amdgcn_fmed3f(a1[pg][c], ka, kb);
+      a1[pg][c] = __builtin_fminf(__builtin_fminf(a1[pg][c], ka), kb);
+      a2[pg][c] = __builtin_fminf(a2[pg][c], tm);
+    };
+    Frag fr = load_frag(0, 0);
+    auto overlapped = [&](Acc& cur, int blk, int nblk, const Acc& prev) {
+      cur = init_acc(blk);
+#pragma unroll
+      for (int tt = 0; tt < NS; ++tt) {
+        const Frag nx = (tt + 1 < NS) ? load_frag(blk, tt + 1) : load_frag(blk + 1 < nblk ? blk + 1 : blk, 0);
+        mfma_step(cur, fr, tt);
+        if constexpr (T2) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (u * NS / 8 == tt) key_pair(prev, u);
+        } else {
+#pragma unroll
+          for (int u = 0; u < 16; ++u)
+            if (u * NS / 16 == tt) key_update(prev, u);
+        }
+        fr = nx;
+      }
+    };
+
+    for (int ch = 0; ch < nchunks; ++ch) {
+      if (nchunks > 1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces (see k_assign_mfma)
+        __syncthreads();
+        point_at(cbuf);
+        if (ch + 1 < nchunks)
+          stage_async(ch + 1, cbuf ^ 1);
+        else if (wt + gridDim.x < nwt)
+          stage_async(0, cbuf ^ 1);
+        cbuf ^= 1;
+        fr = load_frag(0, 0);
+      }
+      const int nb = min(KC, kp - ch * KC) / 32;  // even
+      const uint32_t jq0 = (uint32_t)((ch * KC) >> 2);
+      Acc accA = init_acc(0), accB;
+#pragma unroll
+      for (int tt = 0; tt < NS; ++tt) {
+        const Frag nx = (tt + 1 < NS) ? load_frag(0, tt + 1) : load_frag(1, 0);
+        mfma_step(accA, fr, tt);
+        fr = nx;
+      }
+      int blk = 1;
+      for (; blk + 1 < nb; blk += 2) {
+        set_jg(jq0 + 8u * (uint32_t)(blk - 1));
+        overlapped(accB, blk, nb, accA);
+        set_jg(jq0 + 8u * (uint32_t)blk);
+        overlapped(accA, blk + 1, nb, accB);
+      }
+      set_jg(jq0 + 8u * (uint32_t)(blk - 1));
+      overlapped(accB, blk, nb, accA);
+      set_jg(jq0 + 8u * (uint32_t)blk);
+      if constexpr (T2) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) key_pair(accB, u);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) key_update(accB, u);
+      }
+    }
+    if (nchunks > 1 && tile >= ntiles) continue;
+
+    // per row group: this lane's 4 chains merged, full indices of the best two
+    auto idx = [&](float v, int c) { return ((__float_as_uint(v) & maskq) << 2) | (uint32_t)c; };
+    float g1[2], g2[2], g3[2];
+    uint32_t gp1[2], gp2[2];
+#pragma unroll
+    for (int pg = 0; pg < 2; ++pg) {
+      float k1 = FLT_MAX, k2 = FLT_MAX, k3 = FLT_MAX;
+      uint32_t p1 = 0, p2 = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        top3p_insert(k1, k2, k3, p1, p2, a1[pg][c], idx(a1[pg][c], c));
+        top3p_insert(k1, k2, k3, p1, p2, a2[pg][c], idx(a2[pg][c], c));
+        top3p_insert(k1, k2, k3, p1, p2, T2 ? a2[pg][c] : a3[pg][c], 0u);
+      }
+      g1[pg] = k1;
+      g2[pg] = k2;
+      g3[pg] = k3;
+      gp1[pg] = p1;
+      gp2[pg] = p2;
+    }
+    float k1, k2, k3;
+    uint32_t p1, p2;
+    {  // reduce-scatter over the lane halves, then the quarter pairs (lower lane's side first)
+      uint32_t K1, Q1, K2, Q2, K3, Q3, P1, R1, P2, R2;
+      swap_halves(__float_as_uint(g1[0]), __float_as_uint(g1[1]), K1, Q1);
+      swap_halves(__float_as_uint(g2[0]), __float_as_uint(g2[1]), K2, Q2);
+      swap_halves(__float_as_uint(g3[0]), __float_as_uint(g3[1]), K3, Q3);
+      swap_halves(gp1[0], gp1[1], P1, R1);
+      swap_halves(gp2[0], gp2[1], P2, R2);
+      k1 = __uint_as_float(K1);
+      k2 = __uint_as_float(K2);
+      k3 = __uint_as_float(K3);
+      p1 = P1;
+      p2 = P2;
+      top3p_insert(k1, k2, k3, p1, p2, __uint_as_float(Q1), R1);
+      top3p_insert(k1, k2, k3, p1, p2, __uint_as_float(Q2), R2);
+      top3p_insert(k1, k2, k3, p1, p2, __uint_as_float(Q3), 0u);
+    }
+    {
+      uint32_t K1, Q1, K2, Q2, K3, Q3, P1, R1, P2, R2;
+      perm_quarters(__float_as_uint(k1), K1, Q1);
+      perm_quarters(__float_as_uint(k2), K2, Q2);
+      perm_quarters(__float_as_uint(k3), K3, Q3);
+      perm_quarters(p1, P1, R1);
+      perm_quarters(p2, P2, R2);
+      k1 = __uint_as_float(K1);
+      k2 = __uint_as_float(K2);
+      k3 = __uint_as_float(K3);
+      p1 = P1;
+      p2 = P2;
+      top3p_insert(k1, k2, k3, p1, p2, __uint_as_float(Q1), R1);
+      top3p_insert(k1, k2, k3, p1, p2, __uint_as_float(Q2), R2);
+      top3p_insert(k1, k2, k3, p1, p2, __uint_as_float(Q3), 0u);
+    }
+    const float xn = sqrtf(xx[pgo]) * 1.0001f;
+    const float B0 = screen_b0(xn, cm, pm, DP, 1);
+    const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k3));
+    const float thr2 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k2));
+    uint32_t kind = 0;
+    bool same_chain = false;
+    if constexpr (T2) {
+      same_chain = ((p1 ^ p2) & 15u) == 0u;  // chain (j & 3, quarter): j & 15
+      if (!(k2 - k1 > thr2)) kind = (same_chain || !(k3 - k1 > thr3)) ? 2u : 1u;
+    } else {
+      if (!(k3 - k1 > thr3))
+        kind = 2;
+      else if (!(k2 - k1 > thr2))
+        kind = 1;
+    }
+    float u1 = FLT_MAX;
+    if (__ballot(kind != 0u) != 0ull && kind != 0u) {
+      const KeyBounds kb = key_bounds(xn, *A.xabs * s, DP, rho, 1);
+      u1 = kb.upper(k1);
+      if (u1 < kb.lower(k2))
+        kind = 0u;
+      else if (kind == 2u && !same_chain && kb.lower(k3) > u1)
+        kind = 1u;
+    }
+    // Candidate lists (kind 4), as in k_assign_mfma: the row's 16 chains
+    // are spread over the four quarter lanes of its column, each holding
+    // them for both row groups; every lane lists the kept keys of its own
+    // chains that may be the argmin of either row, then the owner lanes
+    // gather the four quarters' lists of their row.
+    if (A.cand != nullptr && __ballot(kind == 2u) != 0ull) {
+      // the other row group's k1, u1, B0 and kind from its owner lanes
+      uint32_t k1o[2], u1o[2], b0o[2], kdo[2];
+      perm_halves(__float_as_uint(k1), k1o[0], k1o[1]);
+      perm_halves(__float_as_uint(u1), u1o[0], u1o[1]);
+      perm_halves(__float_as_uint(B0), b0o[0], b0o[1]);
+      perm_halves(kind, kdo[0], kdo[1]);
+      // per row group: that row's bound state, for this lane's chains
+      KeyBounds kbg[2];
+      bool act[2], over[2];
+#pragma unroll
+      for (int pg = 0; pg < 2; ++pg) {
+        act[pg] = kdo[pg] == 2u;
+        kbg[pg] = key_bounds(sqrtf(xx[pg]) * 1.0001f, *A.xabs * s, DP, rho, 1);
+        const float K1 = __uint_as_float(k1o[pg]);
+        over[pg] = act[pg] && (!(K1 == K1) || !(fabsf(K1) < 3.0e38f));
+      }
+      auto maybe = [&](float v, int pg) {  // v's centroid may be row pg's argmin (NaN: yes)
+        const float K1 = __uint_as_float(k1o[pg]), U1 = __uint_as_float(u1o[pg]), BB = __uint_as_float(b0o[pg]);
+        return act[pg] && !(v - K1 > 2.0f * BB + rho * (fabsf(K1) + fabsf(v))) && !(kbg[pg].lower(v) > U1);
+      };
+      // the owner's row collects the kept keys of the row's 16 chains (its
+      // own quarter and the other three), in ascending order: each value is
+      // bubbled into a sorted list of CAND_REC - 1 (np.argmin's tie-break in
+      // k_rerank2; indices are distinct)
+      uint32_t srt[CAND_REC - 1];
+#pragma unroll
+      for (int i = 0; i < CAND_REC - 1; ++i) srt[i] = 0xffffffffu;
+      int nc = 0;
+      auto collect = [&](uint32_t c0v, uint32_t c1v) {  // this lane's entry for row groups 0 and 1
+        uint32_t h0, h1, w[4];
+        swap_halves(c0v, c1v, h0, h1);
+        perm_quarters(h0, w[0], w[1]);
+        perm_quarters(h1, w[2], w[3]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool ok = w[e] < (uint32_t)A.k;
+          nc += ok;
+          uint32_t x = ok ? w[e] : 0xffffffffu;
+#pragma unroll
+          for (int i = 0; i < CAND_REC - 1; ++i) {
+            const uint32_t lo = min(srt[i], x), hi = max(srt[i], x);
+            srt[i] = lo;
+            x = hi;
+          }
+        }
+      };
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+#pragma unroll
+        for (int pg = 0; pg < 2; ++pg) over[pg] |= maybe(T2 ? a2[pg][c] : a3[pg][c], pg);
+        collect(maybe(a1[0][c], 0) ? idx(a1[0][c], c) : 0xffffffffu, maybe(a1[1][c], 1) ? idx(a1[1][c], c) : 0xffffffffu);
+        if constexpr (!T2)
+          collect(maybe(a2[0][c], 0) ? idx(a2[0][c], c) : 0xffffffffu,
+                  maybe(a2[1][c], 1) ? idx(a2[1][c], c) : 0xffffffffu);
+      }
+      uint32_t ov0, ov1, ovq[4];
+      swap_halves((uint32_t)over[0], (uint32_t)over[1], ov0, ov1);
+      perm_quarters(ov0, ovq[0], ovq[1]);
+      perm_quarters(ov1, ovq[2], ovq[3]);
+      const bool overall = (ovq[0] | ovq[1] | ovq[2] | ovq[3]) != 0u;
+      const bool lead = (q & 1) == 0;
+      const bool want = lead && valid && kind == 2u && !overall && nc >= 1 && nc < CAND_REC;
+      const uint64_t m4 = __ballot(want);
+      if (m4) {
+        const int leader = __ffsll((unsigned long long)m4) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(A.cand_ctr, (uint32_t)__popcll(m4));
+        base = __shfl(base, leader);
+        const uint32_t slot = base + (uint32_t)__popcll(m4 & ((1ull << lane) - 1ull));
+        if (want && slot < A.cand_cap) {
+          uint32_t* rec = A.cand + (size_t)slot * CAND_REC;
+          rec[0] = (uint32_t)nc;
+#pragma unroll
+          for (int i = 0; i < CAND_REC - 1; ++i) rec[1 + i] = srt[i];
+          kind = 4u;
+          p2 = slot;
+        }
+      }
+    }
+    const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
+    const bool lead = (q & 1) == 0;  // one lane of each pair (l, l ^ 16) writes
+    if (lead && valid) A.labels[row] = lab;
+    const bool enq = lead && valid && (kind != 0);
+    const uint64_t m = __ballot(enq);
+    if (m) {
+      const uint64_t m1 = __ballot(enq && (kind == 1 || kind == 4));
+      const uint64_t m2 = m & ~m1;
+      const uint64_t below = (1ull << lane) - 1ull;
+      if (enq) {
+        QEntry qe;
+        qe.row = (uint32_t)row;
+        qe.i1 = p1;
+        qe.i2 = p2;
+        qe.kind = kind;
+        const uint32_t pos = (kind == 1 || kind == 4) ? qn + (uint32_t)__popcll(m1 & below)
+                                                      : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
+        wq[pos] = qe;
+      }
+      qn += (uint32_t)__popcll(m1);
+      qf += (uint32_t)__popcll(m2);
+    }
+  }
+  if (lane == 0) {
+    A.qcount[2 * gw] = qn;
+    A.qcount[2 * gw + 1] = qf;
+  }
+}
+
 #ifndef KM_WIDE_FW
 #define KM_WIDE_FW 64
 #endif
@@ -1412,8 +1916,47 @@ static int mfma_top2(int ns) {
   return e >= 0 ? e : (ns <= 2 ? 1 : 0);
 }
 
+// the 16x16x32 screen (k_assign_mfma16) where dp is a multiple of 32;
+// KM_MFMA16=0 builds the 32x32x16 one everywhere (A/B arm, make alt)
+#ifndef KM_MFMA16
+#define KM_MFMA16 1
+#endif
+template <int NS>
+static bool launch_mfma16_ns(int waves, int blocks, size_t lds, hipStream_t s, const MfmaArgs& a) {
+  static const int on = diag_env("KM_MFMA16", KM_MFMA16);
+  if constexpr (NS % 2 != 0 || NS > 8) {
+    return false;
+  } else {
+    if (!on) return false;
+    const bool t2 = mfma_top2(NS);
+    if (waves == 16 && NS <= 4) {
+      if (t2)
+        hipLaunchKernelGGL((k_assign_mfma16<NS, 16, true>), dim3(blocks), dim3(1024), lds, s, a);
+      else
+        hipLaunchKernelGGL((k_assign_mfma16<NS, 16>), dim3(blocks), dim3(1024), lds, s, a);
+    } else if (waves == 12) {
+      if (t2)
+        hipLaunchKernelGGL((k_assign_mfma16<NS, 12, true>), dim3(blocks), dim3(768), lds, s, a);
+      else
+        hipLaunchKernelGGL((k_assign_mfma16<NS, 12>), dim3(blocks), dim3(768), lds, s, a);
+    } else if (waves == 4) {
+      if (t2)
+        hipLaunchKernelGGL((k_assign_mfma16<NS, 4, true>), dim3(blocks), dim3(256), lds, s, a);
+      else
+        hipLaunchKernelGGL((k_assign_mfma16<NS, 4>), dim3(blocks), dim3(256), lds, s, a);
+    } else {
+      if (t2)
+        hipLaunchKernelGGL((k_assign_mfma16<NS, 8, true>), dim3(blocks), dim3(512), lds, s, a);
+      else
+        hipLaunchKernelGGL((k_assign_mfma16<NS, 8>), dim3(blocks), dim3(512), lds, s, a);
+    }
+    return true;
+  }
+}
+
 template <int NS>
 static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, const MfmaArgs& a) {
+  if (launch_mfma16_ns<NS>(waves, blocks, lds, s, a)) return;
   if constexpr (NS <= 4) {
     if (mfma_top2(NS)) {
       if (waves == 4)
@@ -1428,10 +1971,13 @@ static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, con
     }
   }
 #ifdef KM_DIAG
-  if constexpr (NS == 8) {  // KM_ABLATE=11 (no key updates) | 12 (MFMA -> adds) | 13 (no lo reads), c5 shape
+  if constexpr (NS == 8) {  // KM_ABLATE=11 (no key updates) | 12 (MFMA -> adds) | 13 (no lo reads)
+                            // | 15 (no key updates, 16x16x32 MFMAs), c5 shape
     static const int e = diag_env("KM_ABLATE", 0);
-    if (waves == 12 && e >= 11 && e <= 13) {  // instead of the product kernel
-      if (e == 11)
+    if (waves == 12 && e >= 11 && e <= 15 && e != 14) {  // instead of the product kernel
+      if (e == 15)
+        hipLaunchKernelGGL((k_assign_mfma<NS, 12, 4>), dim3(blocks), dim3(768), lds, s, a);
+      else if (e == 11)
         hipLaunchKernelGGL((k_assign_mfma<NS, 12, 1>), dim3(blocks), dim3(768), lds, s, a);
       else if (e == 12)
         hipLaunchKernelGGL((k_assign_mfma<NS, 12, 2>), dim3(blocks), dim3(768), lds, s, a);
@@ -1447,7 +1993,10 @@ static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, con
     if (waves == 4)
       hipLaunchKernelGGL((k_assign_mfma<NS, 4>), dim3(blocks), dim3(256), lds, s, a);
     else if (waves == 16) {
-      if constexpr (NS <= 4) hipLaunchKernelGGL((k_assign_mfma<NS, 16>), dim3(blocks), dim3(1024), lds, s, a);
+      if constexpr (NS <= 4)
+        hipLaunchKernelGGL((k_assign_mfma<NS, 16>), dim3(blocks), dim3(1024), lds, s, a);
+      else  // no 16-wave instance past dp 64 (spills): the 8-wave one, never a silent no-launch
+        hipLaunchKernelGGL((k_assign_mfma<NS, 8>), dim3(blocks), dim3(512), lds, s, a);
     } else if (waves == 12)
       hipLaunchKernelGGL((k_assign_mfma<NS, 12>), dim3(blocks), dim3(768), lds, s, a);
     else
@@ -1611,12 +2160,6 @@ struct FusedArgs {
 
 constexpr int ceil_log2_c(int v) { return v <= 1 ? 0 : 1 + ceil_log2_c((v + 1) / 2); }
 
-__device__ __forceinline__ void perm_halves(uint32_t v, uint32_t& lo, uint32_t& hi) {
-  // lo = value of lane (l & 31), hi = value of lane (l | 32), in every lane
-  const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-  lo = p[0];
-  hi = p[1];
-}
 
 // ABL (diagnostic builds, KM_ABLATE=1..4, c3 shape only; results wrong):
 // 1 = no key updates, 2 = no MFMAs, 3 = no LDS sums, 4 = no merge / queue,
@@ -2046,26 +2589,6 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
 // lanes l and l ^ 16 hold the top-3 and best two of row (l & 15) + 16 (l >> 5).
 // The bound is screen_b0's with the 16x16x32 accumulation model (chain_err).
 // ---------------------------------------------------------------------------
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// KM_SWAP_ASM: the swaps as inline asm with two wait states on both sides
-// (A/B of the builtin's code generation)
-#ifndef KM_SWAP_ASM
-#define KM_SWAP_ASM 0
-#endif
-__device__ __forceinline__ void perm_quarters(uint32_t v, uint32_t& lo, uint32_t& hi) {
-  // lo = value of lane (l & ~16), hi = value of lane (l | 16), in every lane
-#if KM_SWAP_ASM
-  lo = v;
-  hi = v;
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(lo), "+v"(hi));
-#else
-  const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-  lo = p[0];
-  hi = p[1];
-#endif
-}
-
 template <int NS2, int NB, bool STATS, bool REF = true, bool SSE = false>
 __global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
   if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
@@ -2271,17 +2794,7 @@ __global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
     // reduce-scatter over the lane halves: permlane32_swap(group 0, group 1)
     // gives lanes 0-31 group 0 of lanes l and l + 32, lanes 32-63 group 1 of
     // lanes l - 32 and l (the lower lane's side first in both)
-    auto swap_groups = [](uint32_t v0, uint32_t v1, uint32_t& lo, uint32_t& hi) {
-#if KM_SWAP_ASM
-      lo = v0;
-      hi = v1;
-      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(lo), "+v"(hi));
-#else
-      const auto p = __builtin_amdgcn_permlane32_swap(v0, v1, false, false);
-      lo = p[0];
-      hi = p[1];
-#endif
-    };
+    auto swap_groups = [](uint32_t v0, uint32_t v1, uint32_t& lo, uint32_t& hi) { swap_halves(v0, v1, lo, hi); };
     float k1, k2, k3;
     uint32_t p1, p2;
     {
