@@ -93,6 +93,7 @@ SIGNATURES = {
     "km_predict": [_P, _PI32],
     "km_labels": [_P, _PI32],
     "km_profile": [_P, _I32],
+    "km_profile_every": [_P, _I32],
     "km_prof_read": [_P, _I32, _PD, _PI64],
 }
 

@@ -2,12 +2,32 @@
 // and km_runtime.hip (context, memory, C-ABI).  Not part of the public ABI
 // (that is include/kmeans_amd.h).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/kmeans_amd.h"
 
 namespace km {
+
+// Timing of a phase's dominant kernel (bench, km_profile): the events ride in
+// the kernel's own dispatch (hipExtLaunchKernelGGL) instead of two extra
+// packets on the stream (~8 us of stream time per step at c2).  A ProfScope
+// arms them; the next KM_TIMED_LAUNCH consumes them.
+struct LaunchTiming {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local LaunchTiming g_timing;
+#define KM_TIMED_LAUNCH(KERNEL, GRID, BLOCK, LDS, STREAM, ...)                                               \
+  do {                                                                                                     \
+    if (::km::g_timing.start) {                                                                            \
+      hipExtLaunchKernelGGL(KERNEL, GRID, BLOCK, LDS, STREAM, ::km::g_timing.start, ::km::g_timing.stop, 0, \
+                            __VA_ARGS__);                                                                  \
+      ::km::g_timing = ::km::LaunchTiming{};                                                               \
+    } else {                                                                                               \
+      hipLaunchKernelGGL(KERNEL, GRID, BLOCK, LDS, STREAM, __VA_ARGS__);                                    \
+    }                                                                                                      \
+  } while (0)
 
 // Ambiguous-point queue entry written by the screening kernels and consumed
 // by k_resolve (exact float64 re-rank of the reference's np.argmin).

@@ -33,6 +33,8 @@
 
 namespace km {
 
+thread_local LaunchTiming g_timing;
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -608,11 +610,11 @@ hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C
 #define KM_SMALL_CASE(DP_)                                                                                 \
   case DP_:                                                                                                \
     if (want_sse)                                                                                          \
-      hipLaunchKernelGGL((k_assign_small<DP_, true>), dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d, \
-                         g.k, C32, C64, cmax, labels, stats, fuse, R, gate, tail);                         \
+      KM_TIMED_LAUNCH((k_assign_small<DP_, true>), dim3((unsigned)blocks), dim3(256), lds, s, X, g.n, g.d,  \
+                      g.k, C32, C64, cmax, labels, stats, fuse, R, gate, tail);                            \
     else                                                                                                   \
-      hipLaunchKernelGGL((k_assign_small<DP_, false>), dim3((unsigned)blocks), dim3(256), lds, s, X, g.n,     \
-                         g.d, g.k, C32, C64, cmax, labels, stats, fuse, R, gate, tail);                    \
+      KM_TIMED_LAUNCH((k_assign_small<DP_, false>), dim3((unsigned)blocks), dim3(256), lds, s, X, g.n,      \
+                      g.d, g.k, C32, C64, cmax, labels, stats, fuse, R, gate, tail);                       \
     break;
   switch (g.dp) {
     KM_SMALL_CASE(16) KM_SMALL_CASE(32) KM_SMALL_CASE(48) KM_SMALL_CASE(64)
@@ -3261,14 +3263,14 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
     const size_t lds = (size_t)g.kp * 4 + (with_stats ? (size_t)(g.dp + 1) * g.kp * 8 : 0);
     if (mode == KM_SCREEN_FAST1) {
       if (with_stats)
-        hipLaunchKernelGGL((k_fused1<4, 8, 1, true, WAVES>), dim3(nbk), dim3(WAVES * 64), lds, s, a, bal, cmax);
+        KM_TIMED_LAUNCH((k_fused1<4, 8, 1, true, WAVES>), dim3(nbk), dim3(WAVES * 64), lds, s, a, bal, cmax);
       else
-        hipLaunchKernelGGL((k_fused1<4, 8, 1, false, WAVES>), dim3(nbk), dim3(WAVES * 64), lds, s, a, bal, cmax);
+        KM_TIMED_LAUNCH((k_fused1<4, 8, 1, false, WAVES>), dim3(nbk), dim3(WAVES * 64), lds, s, a, bal, cmax);
     } else {
       if (with_stats)
-        hipLaunchKernelGGL((k_fused1<4, 8, 2, true, WAVES>), dim3(nbk), dim3(WAVES * 64), lds, s, a, bal, cmax);
+        KM_TIMED_LAUNCH((k_fused1<4, 8, 2, true, WAVES>), dim3(nbk), dim3(WAVES * 64), lds, s, a, bal, cmax);
       else
-        hipLaunchKernelGGL((k_fused1<4, 8, 2, false, WAVES>), dim3(nbk), dim3(WAVES * 64), lds, s, a, bal, cmax);
+        KM_TIMED_LAUNCH((k_fused1<4, 8, 2, false, WAVES>), dim3(nbk), dim3(WAVES * 64), lds, s, a, bal, cmax);
     }
     return hipGetLastError();
   }
@@ -3303,29 +3305,29 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
 #define KM_FUSED_CASE(NS_, NB_)                                                                        \
   case NS_ * 100 + NB_:                                                                                \
     if (with_stats && sse)                                                                             \
-      hipLaunchKernelGGL((k_fused<NS_, NB_, true, 0, true, true>), dim3(nbk), dim3(256), lds, s, a);   \
+      KM_TIMED_LAUNCH((k_fused<NS_, NB_, true, 0, true, true>), dim3(nbk), dim3(256), lds, s, a);   \
     else if (with_stats && !refine)                                                                    \
-      hipLaunchKernelGGL((k_fused<NS_, NB_, true, 0, false>), dim3(nbk), dim3(256), lds, s, a);        \
+      KM_TIMED_LAUNCH((k_fused<NS_, NB_, true, 0, false>), dim3(nbk), dim3(256), lds, s, a);        \
     else if (with_stats)                                                                               \
-      hipLaunchKernelGGL((k_fused<NS_, NB_, true>), dim3(nbk), dim3(256), lds, s, a);                  \
+      KM_TIMED_LAUNCH((k_fused<NS_, NB_, true>), dim3(nbk), dim3(256), lds, s, a);                  \
     else                                                                                               \
-      hipLaunchKernelGGL((k_fused<NS_, NB_, false>), dim3(nbk), dim3(256), lds, s, a);                 \
+      KM_TIMED_LAUNCH((k_fused<NS_, NB_, false>), dim3(nbk), dim3(256), lds, s, a);                 \
     break;
 #ifdef KM_DIAG
   {
     static const int abl = diag_env("KM_ABLATE", 0);
     if (abl >= 1 && abl <= 10 && ns == 4 && nb == 8 && with_stats && !sse) {
       switch (abl) {
-        case 1: hipLaunchKernelGGL((k_fused<4, 8, true, 1>), dim3(nbk), dim3(256), lds, s, a); break;
-        case 2: hipLaunchKernelGGL((k_fused<4, 8, true, 2>), dim3(nbk), dim3(256), lds, s, a); break;
-        case 3: hipLaunchKernelGGL((k_fused<4, 8, true, 3>), dim3(nbk), dim3(256), lds, s, a); break;
-        case 5: hipLaunchKernelGGL((k_fused<4, 8, true, 5>), dim3(nbk), dim3(256), lds, s, a); break;
-        case 7: hipLaunchKernelGGL((k_fused<4, 8, true, 7>), dim3(nbk), dim3(256), lds, s, a); break;
-        case 8: hipLaunchKernelGGL((k_fused<4, 8, true, 8>), dim3(nbk), dim3(256), lds, s, a); break;
-        case 6: hipLaunchKernelGGL((k_fused<4, 8, true, 6>), dim3(nbk), dim3(256), lds, s, a); break;
-        case 9: hipLaunchKernelGGL((k_fusedp<4, 8, false, true>), dim3(nbk), dim3(256), lds_p, s, a); break;
-        case 10: hipLaunchKernelGGL((k_fusedp<4, 8, false>), dim3(nbk), dim3(256), lds_p, s, a); break;
-        default: hipLaunchKernelGGL((k_fused<4, 8, true, 4>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 1: KM_TIMED_LAUNCH((k_fused<4, 8, true, 1>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 2: KM_TIMED_LAUNCH((k_fused<4, 8, true, 2>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 3: KM_TIMED_LAUNCH((k_fused<4, 8, true, 3>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 5: KM_TIMED_LAUNCH((k_fused<4, 8, true, 5>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 7: KM_TIMED_LAUNCH((k_fused<4, 8, true, 7>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 8: KM_TIMED_LAUNCH((k_fused<4, 8, true, 8>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 6: KM_TIMED_LAUNCH((k_fused<4, 8, true, 6>), dim3(nbk), dim3(256), lds, s, a); break;
+        case 9: KM_TIMED_LAUNCH((k_fusedp<4, 8, false, true>), dim3(nbk), dim3(256), lds_p, s, a); break;
+        case 10: KM_TIMED_LAUNCH((k_fusedp<4, 8, false>), dim3(nbk), dim3(256), lds_p, s, a); break;
+        default: KM_TIMED_LAUNCH((k_fused<4, 8, true, 4>), dim3(nbk), dim3(256), lds, s, a); break;
       }
       return hipGetLastError();
     }
@@ -3336,28 +3338,28 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
     if (pair && NB_ <= 8) {                                                                             \
       KM_FUSED16_PAIR(NS2_, (NB_ <= 8 ? NB_ : 8))                                                       \
     } else if (with_stats && sse)                                                                       \
-      hipLaunchKernelGGL((k_fused16<NS2_, NB_, true, true, true>), dim3(nbk), dim3(256), lds, s, a);    \
+      KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, true, true, true>), dim3(nbk), dim3(256), lds, s, a);    \
     else if (with_stats && !refine)                                                                     \
-      hipLaunchKernelGGL((k_fused16<NS2_, NB_, true, false>), dim3(nbk), dim3(256), lds, s, a);         \
+      KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, true, false>), dim3(nbk), dim3(256), lds, s, a);         \
     else if (with_stats)                                                                                \
-      hipLaunchKernelGGL((k_fused16<NS2_, NB_, true>), dim3(nbk), dim3(256), lds, s, a);                \
+      KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, true>), dim3(nbk), dim3(256), lds, s, a);                \
     else if (KM_F16_PREDICT == 1)                                                                       \
-      hipLaunchKernelGGL((k_fused16<NS2_, NB_, true>), dim3(nbk), dim3(256), lds_s, s, a);              \
+      KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, true>), dim3(nbk), dim3(256), lds_s, s, a);              \
     else if (KM_F16_PREDICT == 2)                                                                       \
-      hipLaunchKernelGGL((k_fused16<NS2_, NB_, false, false>), dim3(nbk), dim3(256), lds, s, a);        \
+      KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, false, false>), dim3(nbk), dim3(256), lds, s, a);        \
     else                                                                                                \
-      hipLaunchKernelGGL((k_fused16<NS2_, NB_, false>), dim3(nbk), dim3(256), lds, s, a);               \
+      KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, false>), dim3(nbk), dim3(256), lds, s, a);               \
     break;
 // the pair screen's instances (KP <= 256)
 #define KM_FUSED16_PAIR(NS2_, NB_)                                                                      \
   if (with_stats && sse)                                                                                \
-    hipLaunchKernelGGL((k_fused16<NS2_, NB_, true, true, true, true>), dim3(nbk), dim3(256), lds + lds_pair, s, a);  \
+    KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, true, true, true, true>), dim3(nbk), dim3(256), lds + lds_pair, s, a);  \
   else if (with_stats && !refine)                                                                       \
-    hipLaunchKernelGGL((k_fused16<NS2_, NB_, true, false, false, true>), dim3(nbk), dim3(256), lds + lds_pair, s, a); \
+    KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, true, false, false, true>), dim3(nbk), dim3(256), lds + lds_pair, s, a); \
   else if (with_stats)                                                                                  \
-    hipLaunchKernelGGL((k_fused16<NS2_, NB_, true, true, false, true>), dim3(nbk), dim3(256), lds + lds_pair, s, a);  \
+    KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, true, true, false, true>), dim3(nbk), dim3(256), lds + lds_pair, s, a);  \
   else                                                                                                  \
-    hipLaunchKernelGGL((k_fused16<NS2_, NB_, false, true, false, true>), dim3(nbk), dim3(256), lds + lds_pair, s, a);
+    KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, false, true, false, true>), dim3(nbk), dim3(256), lds + lds_pair, s, a);
 #ifndef KM_F16_PREDICT
 #define KM_F16_PREDICT 0
 #endif

@@ -177,6 +177,8 @@ struct km_ctx {
   hipEvent_t staged[2] = {nullptr, nullptr};  // a half's copy has left it
   // profiling
   int prof = 0;                  // bitmask of KM_K_* phases timed with events
+  int prof_period = 1;           // time one launch in prof_period per phase
+  int64_t prof_tick[KM_K_COUNT] = {};
   const double* prep_of = nullptr;  // the centroid buffer the derived images were built from
   // timed launches: events, and the batch / slot of the iteration that
   // enqueued them (a stopped batch's later launches are no-ops: km_batch_end
@@ -207,17 +209,30 @@ namespace {
 struct ProfScope {
   km_ctx* c;
   int kind;
+  bool in_dispatch;  // the events ride in the scope's one timed kernel (KM_TIMED_LAUNCH)
   hipEvent_t a = nullptr, b = nullptr;
-  ProfScope(km_ctx* ctx, int k) : c(ctx), kind(k) {
-    if ((c->prof >> kind) & 1) {
+  bool on;
+  ProfScope(km_ctx* ctx, int k, bool dispatch = false)
+      : c(ctx), kind(k), in_dispatch(dispatch),
+        on(((c->prof >> k) & 1) && (c->prof_tick[k]++ % c->prof_period) == 0) {
+    if (on) {
       a = c->take_event();
       b = c->take_event();
-      (void)hipEventRecord(a, c->stream);
+      if (in_dispatch)
+        km::g_timing = km::LaunchTiming{a, b};
+      else
+        (void)hipEventRecord(a, c->stream);
     }
   }
   ~ProfScope() {
-    if ((c->prof >> kind) & 1) {
-      (void)hipEventRecord(b, c->stream);
+    if (on) {
+      if (!in_dispatch) {
+        (void)hipEventRecord(b, c->stream);
+      } else if (km::g_timing.start) {  // no timed launch happened (n = 0): an empty interval
+        km::g_timing = km::LaunchTiming{};
+        (void)hipEventRecord(a, c->stream);
+        (void)hipEventRecord(b, c->stream);
+      }
       c->ev[kind].push_back({a, b, c->in_batch ? c->batch_seq : -1, c->batch_n});
     }
   }
@@ -396,14 +411,14 @@ int run_assign(km_ctx* c, bool with_stats) {
   if (with_stats && !c->stats_clean) KM_HIP(hipMemsetAsync(c->stats, 0, sizeof(double) * stats_len(g), c->stream));
   if (with_stats) c->stats_clean = false;
   if (c->path == 1) {
-    ProfScope ps(c, KM_K_ASSIGN);
+    ProfScope ps(c, KM_K_ASSIGN, true);
     KM_HIP(km::launch_assign_small(c->X, g, c->C32, c->C64_cur, c->cmax, c->labels, c->stats, with_stats ? 1 : 0,
                                    sse ? 1 : 0, c->n_cu, c->gate, c->stream, small_tail(c)));
     return KM_OK;
   }
   if (c->fused) {
     {
-      ProfScope ps(c, KM_K_ASSIGN);
+      ProfScope ps(c, KM_K_ASSIGN, true);
       KM_HIP(km::launch_fused(c->X, c->xnorm, g, c->Chi, c->Clo, c->ChiF, c->CloF, c->cn2s, c->bnd, c->xabs, c->cabs,
                               c->labels, c->queue, c->qcount, c->stats, with_stats ? 1 : 0,
                               (with_stats || c->screen >= km::KM_SCREEN_FAST1) ? c->screen : km::KM_SCREEN_X3_REFINE,
@@ -949,7 +964,7 @@ int km_update_async(km_ctx* c, double tol, int64_t empty_seed) {
     t.C32n = fold_prep ? c->C32 : nullptr;
     t.cmaxn = fold_prep ? c->cmax : nullptr;
     {
-      ProfScope ps(c, KM_K_ASSIGN);
+      ProfScope ps(c, KM_K_ASSIGN, true);
       KM_HIP(km::launch_assign_small(c->X, c->g, c->C32, c->C64_cur, c->cmax, c->labels, c->stats, 1,
                                      c->want_sse ? 1 : 0, c->n_cu, c->gate, c->stream, t));
     }
@@ -1262,6 +1277,14 @@ int km_labels(km_ctx* c, int32_t* labels_out) {
 int km_profile(km_ctx* c, int32_t enable) {
   KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
   c->prof = enable;  // bitmask of (1 << KM_K_*); -1 = every phase
+  return KM_OK;
+}
+
+int km_profile_every(km_ctx* c, int32_t period) {
+  KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
+  KM_REQUIRE(period >= 1, KM_ERR_ARG, "km_profile_every: period must be >= 1");
+  c->prof_period = period;
+  for (auto& t : c->prof_tick) t = 0;
   return KM_OK;
 }
 

@@ -265,13 +265,15 @@ class HipEngine:
     # -- profiling ---------------------------------------------------------------
     _PHASES = {"assign": 0, "resolve": 1, "stats": 2, "update": 3, "prep": 4}   # KM_K_* (kmeans_amd.h)
 
-    def profile(self, enable: bool = True, phases=None) -> None:
+    def profile(self, enable: bool = True, phases=None, every: int = 1) -> None:
         """Time launches with HIP events: every phase, or only ``phases``
-        (names of ``_PHASES``).  Each event record costs a few microseconds of
-        stream time, so a timed region records only the phases it reports."""
+        (names of ``_PHASES``), one launch in ``every`` of each.  Each timed
+        launch costs a few microseconds of stream time, so a timed region
+        records only the phases it reports."""
         mask = 0
         if enable:
             mask = -1 if phases is None else sum(1 << self._PHASES[p] for p in phases)
+        self._c(self.lib.km_profile_every(self.ctx, int(every)), "km_profile_every")
         self._c(self.lib.km_profile(self.ctx, mask), "km_profile")
 
     def prof_read(self, kind: str) -> Tuple[float, int]:

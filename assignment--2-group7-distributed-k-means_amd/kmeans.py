@@ -93,7 +93,9 @@ class LloydRunner:
         that ran exactly as ``iteration`` does.  Returns True on convergence."""
         it = first
         eng = self.engine
-        size = self.batch
+        # the batch size carries over between calls on one runner (a caller
+        # running the loop in pieces, like bench.py's warmup and timed region)
+        size = getattr(self, "_next_batch", self.batch)
         while it < max_iter:
             m = min(size, max_iter - it)
             # the repair seed of each iteration, int(time.time()) read per
@@ -127,6 +129,7 @@ class LloydRunner:
             # a batch that ran through doubles the next one (fewer host round
             # trips on long runs); a stopped one (convergence, empties) resets it
             size = min(2 * size, _lib.KM_MAX_BATCH) if len(recs) == m and not recs[-1][0].stop_reason else self.batch
+            self._next_batch = size
             for b, (st, counts) in enumerate(recs):
                 if b + 1 < len(recs):                          # ran through: committed on the device
                     self._record(model, it, st, counts, st.max_shift, log)

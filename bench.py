@@ -173,7 +173,9 @@ def main():
     # events only around the dominant kernel inside the timed region (each
     # record costs a few us of stream time); the other phases' durations come
     # from two untimed steps after it
-    eng.profile(True, phases=("assign", "stats"))
+    # (one launch in 4 on the sub-millisecond steps of c1/c2, where each timed
+    # launch's ~6 us of stream time would be 4% of the step)
+    eng.profile(True, phases=("assign", "stats"), every=4 if args.config in ("c1", "c2") else 1)
     ran0 = run.iterations_ran
     t0 = time.perf_counter()
     run.run(km, log, args.warmup + args.steps, first=args.warmup)
@@ -185,7 +187,7 @@ def main():
     # early only on convergence (max_shift < 1e-300, i.e. an exact fixed
     # point), empties or NaN; the rate counts what ran, never args.steps
     ran = run.iterations_ran - ran0
-    eng.profile(True, phases=("resolve", "update", "prep"))
+    eng.profile(True, phases=("resolve", "update", "prep"), every=1)
     run.run(km, log, args.warmup + args.steps + 2, first=args.warmup + args.steps)
     eng.sync()
     eng.profile(False)

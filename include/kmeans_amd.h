@@ -230,6 +230,9 @@ int km_get_screen(km_ctx* ctx, int32_t* mode);
 /* Kernel timing with HIP events on the context stream.  `enable` is a
  * bitmask of (1 << KM_K_*) phases to time (-1: all, 0: off). */
 int km_profile(km_ctx* ctx, int32_t enable);
+/* Time one launch in `period` (>= 1, default 1) of each profiled phase: each
+ * timed launch costs ~6 us of stream time, which a 0.16 ms c2 step notices. */
+int km_profile_every(km_ctx* ctx, int32_t period);
 int km_prof_read(km_ctx* ctx, int32_t kind, double* total_ms, int64_t* launches);
 
 #ifdef __cplusplus
