@@ -3350,6 +3350,10 @@ bool fused16_ok(const Geometry& g) {
 }
 
 bool pair_ok(const Geometry& g) {
+#if !KM_PAIR && !defined(KM_DIAG)
+  (void)g;
+  return false;  // not built (launch_fused's KM_PAIR_BRANCH)
+#endif
   static const int on = diag_env("KM_PAIR", KM_PAIR);
   return on && fused16_ok(g) && g.kp <= 256 &&
          (size_t)g.kp * 4 + (size_t)(g.dp + 1) * g.kp * 8 + (size_t)g.kp * (KM_PAIR_M + 1) * 4 <= 160 * 1024;
@@ -3420,7 +3424,7 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
   FusedArgs a{X, xnorm, g.n, g.k, g.d, seg, ChiF, CloF, cn2s, bnd, xabs, cabs, labels, queue, qcount, stats, gate,
                 C64P, sse, pairs};
   const size_t lds = (size_t)g.kp * 4 + (with_stats ? (size_t)(g.dp + 1) * g.kp * 8 : 0);
-  const size_t lds_pair = (size_t)g.kp * (KM_PAIR_M + 1) * 4;
+  [[maybe_unused]] const size_t lds_pair = (size_t)g.kp * (KM_PAIR_M + 1) * 4;
 #ifdef KM_DIAG
   const size_t lds_p = (size_t)g.kp * 4 + (size_t)(g.dp + 1) * (g.kp + 1) * 8;  // k_fusedp: discard column
 #endif
@@ -3457,9 +3461,8 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
 #endif
 #define KM_FUSED16_CASE(NS2_, NB_)                                                                      \
   case NS2_ * 100 + NB_:                                                                                \
-    if (pair && NB_ <= 8) {                                                                             \
-      KM_FUSED16_PAIR(NS2_, (NB_ <= 8 ? NB_ : 8))                                                       \
-    } else if (with_stats && sse)                                                                       \
+    KM_PAIR_BRANCH(NS2_, NB_)                                                                           \
+    if (with_stats && sse)                                                                              \
       KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, true, true, true>), dim3(nbk), dim3(256), lds, s, a);    \
     else if (with_stats && !refine)                                                                     \
       KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, true, false>), dim3(nbk), dim3(256), lds, s, a);         \
@@ -3472,7 +3475,16 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
     else                                                                                                \
       KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, false>), dim3(nbk), dim3(256), lds, s, a);               \
     break;
-// the pair screen's instances (KP <= 256)
+// the pair screen's instances (KP <= 256): built with -DKM_PAIR=1 and in the
+// diagnostic library (env KM_PAIR=1) only, since it lost end to end
+#if KM_PAIR || defined(KM_DIAG)
+#define KM_PAIR_BRANCH(NS2_, NB_)                                                                       \
+  if (pair && NB_ <= 8) {                                                                               \
+    KM_FUSED16_PAIR(NS2_, (NB_ <= 8 ? NB_ : 8))                                                         \
+  } else
+#else
+#define KM_PAIR_BRANCH(NS2_, NB_)
+#endif
 #define KM_FUSED16_PAIR(NS2_, NB_)                                                                      \
   if (with_stats && sse)                                                                                \
     KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, true, true, true, true>), dim3(nbk), dim3(256), lds + lds_pair, s, a);  \
@@ -3499,6 +3511,7 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
   }
 #undef KM_FUSED16_CASE
 #undef KM_FUSED16_PAIR
+#undef KM_PAIR_BRANCH
   switch (ns * 100 + nb) {
     KM_FUSED_CASE(4, 2) KM_FUSED_CASE(4, 4) KM_FUSED_CASE(4, 6) KM_FUSED_CASE(4, 8)
     KM_FUSED_CASE(2, 2) KM_FUSED_CASE(2, 4) KM_FUSED_CASE(2, 6) KM_FUSED_CASE(2, 8) KM_FUSED_CASE(2, 12)
