@@ -317,22 +317,6 @@ __device__ void update_one_body(double* __restrict__ stats, const double* __rest
 #ifndef KM_SMALL_WPE
 #define KM_SMALL_WPE 4
 #endif
-#ifndef KM_SMALL_PF2
-#define KM_SMALL_PF2 0
-#endif
-// expanded-form screen on the small path (A/B)
-#ifndef KM_SMALL_EXP
-#define KM_SMALL_EXP 0
-#endif
-// coalesced row loads through an LDS stage on the small path (A/B)
-#ifndef KM_SMALL_COAL
-#define KM_SMALL_COAL 0
-#endif
-// byte offset of the dp = 16 row stage in k_assign_small's LDS: centroids,
-// statistics replicas, wave queues, ||c||^2
-__host__ __device__ inline size_t small_stage_off(int k, int dp, int d1, int R) {
-  return ((size_t)k * dp * 4 + 15) / 16 * 16 + (size_t)k * d1 * 8 * R + (size_t)4 * 32 * 4 + (size_t)32 * 4;
-}
 template <int DP, bool SSE, int WPE = (DP <= 16 ? KM_SMALL_WPE : 1)>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const float* __restrict__ C32,
@@ -354,17 +338,6 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
   for (int i = threadIdx.x; i < k * DP; i += blockDim.x) sC[i] = C32[i];
   if (fuse)
     for (int i = threadIdx.x; i < k * d1 * R; i += blockDim.x) tab[i] = 0.0;
-  // expanded form: ||c'_j||^2 (float64 sum, one rounding), after the wave queues
-  float* sCn = reinterpret_cast<float*>(smem + ((k * DP * 4 + 15) / 16) * 16 + (fuse ? (size_t)k * d1 * R * 8 : 0) +
-                                        (size_t)4 * SMALL_QW * 4);
-  if (KM_SMALL_EXP && threadIdx.x < k) {
-    double nn = 0.0;
-    for (int f = 0; f < DP; ++f) {
-      const double c = (double)C32[(size_t)threadIdx.x * DP + f];
-      nn = fma(c, c, nn);
-    }
-    sCn[threadIdx.x] = (float)nn;
-  }
   __syncthreads();
 
   const int b = ceil_log2(k);
@@ -389,11 +362,8 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
   // (at 8 waves per SIMD the other waves hide the latency instead: no
   // prefetch, 2 dp fewer VGPRs)
   constexpr bool PF = WPE < 8;
-  // PF2 (KM_SMALL_PF2, dp = 16): two rows in flight per lane instead of one
-  constexpr bool PF2 = PF && KM_SMALL_PF2 && DP <= 16;
-  constexpr bool COAL = KM_SMALL_COAL && DP == 16;
   float4 nx[DP / 4];
-  if (PF && !COAL && row < n) {
+  if (PF && row < n) {
 #pragma unroll
     for (int f = 0; f < DP; f += 4) nx[f / 4] = *reinterpret_cast<const float4*>(X + row * DP + f);
   }
@@ -401,35 +371,7 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
     float k1 = FLT_MAX, k2 = FLT_MAX, k3 = FLT_MAX;
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     bool amb;
-    if constexpr (KM_SMALL_EXP) {
-      // expanded form s_j = ||c'_j||^2 - 2 c'_j.x: half the VALU of the direct
-      // form (one v_pk_fma_f32 per feature pair and centroid).  Its error is
-      // relative to ||x|| ||c||, not to the distance: per row
-      //   |s~_j - S_j| <= E = (DP + 8) u (2 X cm + cm^2) + 2 u cm (cm + X)
-      // (two fma chains of DP/2 terms, their sum, the final fma, ||c'||^2's
-      // rounding, and the float64 -> fp32 rounding of c), X >= ||x||
-      f32x2 xx2 = {0.0f, 0.0f};
-#pragma unroll
-      for (int f = 0; f < DP; f += 2) {
-        const f32x2 xv = {x[f], x[f + 1]};
-        xx2 = __builtin_elementwise_fma(xv, xv, xx2);
-      }
-      const float X = sqrtf((xx2.x + xx2.y) * (1.0f + 64.0f * U24)) * (1.0f + 2.0f * U24);
-#pragma unroll 2
-      for (int j = 0; j < k; ++j) {
-        const f32x2* c2 = reinterpret_cast<const f32x2*>(sC + j * DP);
-        f32x2 acc2 = {0.0f, 0.0f};
-#pragma unroll
-        for (int f = 0; f < DP; f += 2) {
-          const f32x2 xv = {x[f], x[f + 1]};
-          acc2 = __builtin_elementwise_fma(xv, c2[f / 2], acc2);
-        }
-        top3_insert(k1, k2, k3, key_of(fmaf(-2.0f, acc2.x + acc2.y, sCn[j]), (uint32_t)j, mask));
-      }
-      const float E = (float)(DP + 8) * U24 * (2.0f * X * cm + cm * cm) + 2.0f * U24 * cm * (cm + X);
-      const float rho = __builtin_ldexpf(1.0f, b - 23) * 1.01f;  // key_of's index bits
-      amb = (k >= 2) && !(k2 - k1 > (2.0f * E + rho * (fabsf(k1) + fabsf(k2))) * 1.0001f);
-    } else {
+    {
       // packed fp32 (v_pk_add_f32 / v_pk_fma_f32): even and odd features in
       // two partial sums, half the VALU issue of the scalar loop; the
       // direct-form bound (DP sequential terms) covers two sums of DP / 2
@@ -504,67 +446,17 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
 #pragma unroll
     for (int f = 0; f < DP; f += 4) v[f / 4] = *reinterpret_cast<const float4*>(X + r * DP + f);
   };
-  if constexpr (COAL) {
-    // coalesced loads (KM_SMALL_COAL, dp = 16): the wave's 64 rows (4 KiB) as
-    // four fully contiguous 1-KiB loads, transposed through this wave's LDS
-    // stage (row stride 20 floats: b128 reads conflict-free) so that each lane
-    // still owns one row; the next chunk loads while this one is processed
-    float* stg = reinterpret_cast<float*>(smem + small_stage_off(k, DP, d1, fuse ? R : 0)) + (threadIdx.x >> 6) * 64 * 20;
-    const int64_t wb0 = row - lane;
-    auto cload = [&](float4 (&v)[4], int64_t wb) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t r = wb + 16 * i + (lane >> 2);
-        v[i] = r < n ? *reinterpret_cast<const float4*>(X + wb * 16 + i * 256 + lane * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-    };
-    float4 cv[4];
-    if (wb0 < n) cload(cv, wb0);
-    for (int64_t wb = wb0; wb < n; wb += rstride) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(stg + (16 * i + (lane >> 2)) * 20 + (lane & 3) * 4) = cv[i];
-      if (wb + rstride < n) cload(cv, wb + rstride);
-      float x[DP];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = *reinterpret_cast<const float4*>(stg + lane * 20 + 4 * q);
-        x[4 * q] = v.x;
-        x[4 * q + 1] = v.y;
-        x[4 * q + 2] = v.z;
-        x[4 * q + 3] = v.w;
-      }
-      if (wb + lane < n) row_body(x, wb + lane);
-    }
-  } else if constexpr (PF2) {
-    // two rows in flight per lane: while row r is processed, r + stride and
-    // r + 2 stride are loading (the loop unrolled by two, no register copies
-    // that would wait on the younger load)
-    float4 nb[DP / 4];
-    if (row + rstride < n) load_row(nb, row + rstride);
-    for (; row < n; row += 2 * rstride) {
-      float x[DP];
+  for (; row < n; row += rstride) {
+    float x[DP];
+    if constexpr (PF) {
       unpack(nx, x);
-      if (row + 2 * rstride < n) load_row(nx, row + 2 * rstride);
-      row_body(x, row);
-      if (row + rstride >= n) break;
-      float y[DP];
-      unpack(nb, y);
-      if (row + 3 * rstride < n) load_row(nb, row + 3 * rstride);
-      row_body(y, row + rstride);
+      if (row + rstride < n) load_row(nx, row + rstride);
+    } else {
+      float4 v[DP / 4];
+      load_row(v, row);
+      unpack(v, x);
     }
-  } else {
-    for (; row < n; row += rstride) {
-      float x[DP];
-      if constexpr (PF) {
-        unpack(nx, x);
-        if (row + rstride < n) load_row(nx, row + rstride);
-      } else {
-        float4 v[DP / 4];
-        load_row(v, row);
-        unpack(v, x);
-      }
-      row_body(x, row);
-    }
+    row_body(x, row);
   }
   // A queued row, resolved by one wave, lanes over centroids: the
   // reference's float64 norms (kmeans_spark.py:153) in NumPy's pairwise
@@ -723,8 +615,7 @@ hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C
   if (!tail.queue || !tail.qctr || !tail.done) return hipErrorInvalidValue;
   const int R = small_replicas(g);
   const size_t lds = ((size_t)g.k * g.dp * 4 + 15) / 16 * 16 + (fuse ? (size_t)g.k * (g.d + 1) * 8 * R : 0) +
-                     (size_t)4 * SMALL_QW * 4 + (size_t)SMALL_MAX_K * 4 +
-                     ((KM_SMALL_COAL && g.dp == 16) ? (size_t)4 * 64 * 20 * 4 : 0);
+                     (size_t)4 * SMALL_QW * 4;
   int64_t blocks = (g.n + 255) / 256;
   static const int bpc = diag_env("KM_SMALL_BPC", KM_SMALL_BPC);
   const int64_t cap = (int64_t)n_cu * bpc;
