@@ -12,6 +12,7 @@
 #include "km_internal.h"
 
 #include <float.h>
+#include <algorithm>
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -26,6 +27,10 @@
 // pair screen (k_fused16): neighbour-list length per centroid, and the switch
 #ifndef KM_PAIR_M
 #define KM_PAIR_M 16
+#endif
+// k_rerank2 runs on n_cu / KM_RERANK_DIV workgroups
+#ifndef KM_RERANK_DIV
+#define KM_RERANK_DIV 1
 #endif
 #ifndef KM_PAIR
 #define KM_PAIR 0
@@ -3909,11 +3914,15 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   const size_t tab_bytes = (size_t)(g.d + 1) * g.kp * 8;
   const size_t pres = (stats ? 2 : 1) * pre_bytes;
   const int tab_kp = (stats && tab_bytes + pres <= LDS_MAX) ? g.kp : 0;
+  // workgroups of the re-rank: each flushes its [k][d+1] table with global
+  // atomics, so fewer workgroups flush fewer (KM_RERANK_DIV: n_cu / div)
+  static const int rdiv = diag_env("KM_RERANK_DIV", KM_RERANK_DIV);
+  const int rwg = std::max(1, n_cu / std::max(1, rdiv));
   if (g.d > 256)
-    hipLaunchKernelGGL(k_rerank2<true>, dim3(n_cu), dim3(512), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
+    hipLaunchKernelGGL(k_rerank2<true>, dim3(rwg), dim3(512), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
                        g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap);
   else
-    hipLaunchKernelGGL(k_rerank2<false>, dim3(n_cu), dim3(1024), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
+    hipLaunchKernelGGL(k_rerank2<false>, dim3(rwg), dim3(1024), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
                        g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap);
   return hipGetLastError();
 }
