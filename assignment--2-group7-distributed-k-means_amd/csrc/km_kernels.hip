@@ -28,9 +28,9 @@
 #ifndef KM_PAIR_M
 #define KM_PAIR_M 16
 #endif
-// k_rerank2 runs on n_cu / KM_RERANK_DIV workgroups
-#ifndef KM_RERANK_DIV
-#define KM_RERANK_DIV 1
+// k_rerank2 runs on KM_RERANK_PCT percent of n_cu workgroups
+#ifndef KM_RERANK_PCT
+#define KM_RERANK_PCT 100
 #endif
 #ifndef KM_PAIR
 #define KM_PAIR 0
@@ -3914,10 +3914,12 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   const size_t tab_bytes = (size_t)(g.d + 1) * g.kp * 8;
   const size_t pres = (stats ? 2 : 1) * pre_bytes;
   const int tab_kp = (stats && tab_bytes + pres <= LDS_MAX) ? g.kp : 0;
-  // workgroups of the re-rank: each flushes its [k][d+1] table with global
-  // atomics, so fewer workgroups flush fewer (KM_RERANK_DIV: n_cu / div)
-  static const int rdiv = diag_env("KM_RERANK_DIV", KM_RERANK_DIV);
-  const int rwg = std::max(1, n_cu / std::max(1, rdiv));
+  // workgroups of the re-rank, in percent of n_cu (KM_RERANK_PCT).  Each
+  // flushes its [k][d+1] table with global atomics, but fewer workgroups lose
+  // more in parallelism than they save (c3 resolve 0.32-0.35 ms at 100%,
+  // 0.48 at 50%, 0.80 at 25%)
+  static const int rpct = diag_env("KM_RERANK_PCT", KM_RERANK_PCT);
+  const int rwg = std::max(1, n_cu * std::max(1, rpct) / 100);
   if (g.d > 256)
     hipLaunchKernelGGL(k_rerank2<true>, dim3(rwg), dim3(512), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
                        g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap);
