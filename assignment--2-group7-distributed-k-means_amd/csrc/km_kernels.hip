@@ -2601,8 +2601,8 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
 }
 
 // ---------------------------------------------------------------------------
-// k_fused16: k_fused on v_mfma_f32_16x16x32_f16 ("MFMA
-// shape").  Same output tile per wave -- 32 rows x KP centroids per tile,
+// k_fused16: k_fused on v_mfma_f32_16x16x32_f16 ("The
+// 16x16x32 shape").  Same output tile per wave -- 32 rows x KP centroids per tile,
 // fp16x3 scores, images in AGPRs, rows double-buffered in registers -- with
 // 16x16 accumulators: a block of 32 centroids is two 16-centroid halves (cb)
 // times two 16-row groups (pg), 12 NS2 MFMAs of 16 cycles (k_fused: 3 NS of
