@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("KM_LIB") or os.path.join(HERE, "libkmeans_amd.so")
 ROOT = os.path.dirname(HERE)
 HEADER = os.path.join(ROOT, "include", "kmeans_amd.h")
 
-KM_ABI_VERSION = 4
+KM_ABI_VERSION = 5
 KM_OK = 0
 KM_EMPTY = 1
 

@@ -96,6 +96,22 @@ class Communicator:
         self.dist.all_gather(out, t)
         return [o.cpu().numpy()[:s] for o, s in zip(out, sizes)]
 
+    def gather_array(self, arr: np.ndarray, root: int = 0):
+        """Variable-length gather of 1-D arrays to ``root``: the list of every
+        rank's array there, None on the other ranks (predict results to the
+        driver, as Spark's collect())."""
+        if self.world == 1:
+            return [np.asarray(arr)]
+        arr = np.ascontiguousarray(arr)
+        sizes = self.allgather_int(arr.shape[0])
+        m = max(sizes) if sizes else 0
+        pad = np.zeros(max(m, 1), dtype=arr.dtype)
+        pad[:arr.shape[0]] = arr
+        t = self._tensor(pad)
+        out = [t.clone() for _ in range(self.world)] if self.rank == root else None
+        self.dist.gather(t, out, dst=root)
+        return [o.cpu().numpy()[:s] for o, s in zip(out, sizes)] if self.rank == root else None
+
     def barrier(self):
         if self.world > 1:
             self.dist.barrier()

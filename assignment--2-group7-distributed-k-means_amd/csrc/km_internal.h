@@ -127,10 +127,12 @@ size_t queue_capacity(int64_t n, int n_cu);
 size_t qcount_words(int n_cu);
 bool mfma_path_ok(const Geometry& g);
 // stats != nullptr: also add the resolved points' rows to the partial sums
+// delta: the queued rows still hold their previous labels (k_s1 delta mode);
+// a resolved row whose label changed moves its x between the sums in stats
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
                           double* stats, int n_cu, const int* gate, hipStream_t s, double* sse = nullptr,
-                          const uint32_t* cand = nullptr, uint32_t cand_cap = 0);
+                          const uint32_t* cand = nullptr, uint32_t cand_cap = 0, int delta = 0);
 // Fused assign + partial sums (kp*dp <= 16384 class): fp16 hi image in VGPRs,
 // lo image + float64 sum table in LDS; decided points summed here, queued
 // points (and their counts) by launch_resolve(stats).
@@ -148,6 +150,9 @@ int diag_env(const char* name, int dflt);
 // per-key refinement (X3_REFINE), or the fast screen k_fused1 (one fp16 image,
 // pairwise bound) with the row as one fp16 part (FAST1) or hi + lo (FAST2).
 // Results are exact in every mode; the choice is a cost choice.
+// (mode 4, KM_SCREEN_S1 of kmeans_amd.h: the one-MFMA screen with in-kernel
+// re-scoring and delta statistics, km_screen1.hip; forcing 0 / 1 keeps
+// k_fused16 on every assign)
 enum { KM_SCREEN_X3 = 0, KM_SCREEN_X3_REFINE = 1, KM_SCREEN_FAST1 = 2, KM_SCREEN_FAST2 = 3 };
 bool fast_path_ok(const Geometry& g);
 // C32, cmax: fp32 centroids and max norm (fast screen image); bal: 2 floats of
@@ -217,6 +222,22 @@ hipError_t launch_repair_apply(int* gate, const Geometry& g, const int32_t* empt
 // takeSample's Bernoulli pass, one wave per partition (km_sample.hip)
 hipError_t launch_bernoulli(const uint64_t* seeds, const int64_t* sizes, const int64_t* bases, int nparts,
                             double fraction, int64_t* out, int cp, int32_t* counts, hipStream_t s);
+// One-MFMA screen with in-kernel fp32 re-scoring (km_screen1.hip; the c3
+// class): greedy chain colouring (perm: table index -> centroid), the
+// per-iteration images, and the screen itself (delta: previous labels read,
+// changed rows moved between the float64 sums in `stats`; else labels only)
+bool s1_ok(const Geometry& g);
+size_t s1_table_entries(const Geometry& g);
+hipError_t launch_s1_color(const float* C32, const Geometry& g, int32_t* perm, const int* gate, hipStream_t s);
+hipError_t launch_s1_prep(const double* C64, const float* C32, const Geometry& g, const int32_t* perm,
+                          const float* cmax, const float* xabs, const float* cabs, float* cft, float* cn2o,
+                          uint4* img, float* cst, const int* gate, hipStream_t s);
+hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, const uint4* img, const float* cn2o,
+                     const float* cft, const int32_t* perm, const float* cst, int32_t* labels,
+                     QEntry* queue, uint32_t* qcount, double* stats, int delta, int n_cu, QLayout* ql,
+                     const int* gate, hipStream_t s);
+// delta statistics: mode 1 full += stats, stats = full; mode 0 full = stats
+hipError_t launch_s1_apply(double* stats, double* full, int64_t len, int mode, const int* gate, hipStream_t s);
 hipError_t launch_gen_blobs(float* X, const Geometry& g, int64_t row_offset, int32_t n_centers, float box,
                             float stddev, uint64_t seed, hipStream_t s);
 

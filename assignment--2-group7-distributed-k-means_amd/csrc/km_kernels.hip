@@ -3516,7 +3516,7 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
                                                   const uint32_t* __restrict__ qcount, QLayout ql,
                                                   int32_t* __restrict__ labels, double* __restrict__ stats,
                                                   int tab_kp, double* __restrict__ sse, const int* __restrict__ gate,
-                                                  const uint32_t* __restrict__ cand, uint32_t cand_cap) {
+                                                  const uint32_t* __restrict__ cand, uint32_t cand_cap, int delta) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* tab = reinterpret_cast<double*>(smem);
@@ -3525,7 +3525,7 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
   if (stats && tab_kp)
     for (int i = threadIdx.x; i < (d + 1) * tab_kp; i += blockDim.x) tab[i] = 0.0;
   block_prefix(qcount, 0, ql.nwaves, pre);
-  if (stats) block_prefix(qcount, 1, ql.nwaves, pre1);
+  if (stats && !delta) block_prefix(qcount, 1, ql.nwaves, pre1);
   const uint32_t total = pre[ql.nwaves];
   const int u = threadIdx.x & 7;
   const uint32_t ng = (gridDim.x * blockDim.x) >> 3;
@@ -3599,6 +3599,8 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
       rsq_bad = best;  // the norm (np_norm_d takes the sqrt)
     }
     if (!ok) lab = __shfl(lab, (int)(threadIdx.x & 63) & ~7);
+    // delta statistics (k_s1): the queued row still holds its previous label
+    const int old = delta ? (int)min((uint32_t)labels[q.row], (uint32_t)(k - 1)) : -1;
     if (u == 0) labels[q.row] = lab;
     // SSE (fused path): min_distance ** 2 with the chosen centroid's norm in
     // NumPy's order (kmeans_spark.py:231-233)
@@ -3606,7 +3608,18 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
       const double mn = ok ? mnorm : rsq_bad;
       ss_acc += mn * mn;
     }
-    if (stats) {
+    if (stats && delta) {
+      if (old != lab) {  // the row moves from cluster old to lab
+        for (int f = u; f < d; f += 8) {
+          atomicAdd(stats + (size_t)old * (d + 1) + f, -(double)x[f]);
+          atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)x[f]);
+        }
+        if (u == 0) {
+          atomicAdd(stats + (size_t)old * (d + 1) + d, -1.0);
+          atomicAdd(stats + (size_t)lab * (d + 1) + d, 1.0);
+        }
+      }
+    } else if (stats) {
       for (int f = u; f < d; f += 8) {
         if (tab_kp)
           atomicAdd(tab + (size_t)f * tab_kp + lab, (double)x[f]);
@@ -3621,7 +3634,7 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
       }
     }
   }
-  if (stats) {
+  if (stats && !delta) {
     // rows of the entries k_fullscan resolved (launched first: their labels
     // are final) into the same table -- one global float64 atomic per table
     // entry instead of one per feature per point, which serialised on the
@@ -3676,7 +3689,7 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
                                                    const uint32_t* __restrict__ qcount, QLayout ql,
                                                    int32_t* __restrict__ labels, int ch,
                                                    double* __restrict__ stats, int use_chain, int pair_chain,
-                                                   double* __restrict__ sse, const int* __restrict__ gate) {
+                                                   double* __restrict__ sse, const int* __restrict__ gate, int delta) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sCT = reinterpret_cast<double*>(smem);                                    // [d][ch]
@@ -3744,9 +3757,22 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
         bi = take ? oj : bi;
       }
       const int lab = bi < 0 ? 0 : bi;
+      // delta statistics (k_s1): the queued row still holds its previous label
+      const int old = delta ? (int)min((uint32_t)labels[rows[g]], (uint32_t)(k - 1)) : -1;
       if (lane == 0) labels[rows[g]] = lab;
       if (sse && lane == 0 && bi >= 0) ss_acc += bv * bv;  // min_distance ** 2 (bv: the norm)
-      if (stats) {
+      if (stats && delta) {
+        if (old != lab) {  // the row moves from cluster old to lab
+          for (int f = lane; f < d; f += 64) {
+            atomicAdd(stats + (size_t)old * (d + 1) + f, -(double)xs[g * d + f]);
+            atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)xs[g * d + f]);
+          }
+          if (lane == 0) {
+            atomicAdd(stats + (size_t)old * (d + 1) + d, -1.0);
+            atomicAdd(stats + (size_t)lab * (d + 1) + d, 1.0);
+          }
+        }
+      } else if (stats) {
         for (int f = lane; f < d; f += 64) atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)xs[g * d + f]);
         if (lane == 0) atomicAdd(stats + (size_t)lab * (d + 1) + d, 1.0);  // count
       }
@@ -3882,7 +3908,7 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
                           double* stats, int n_cu, const int* gate, hipStream_t s, double* sse,
-                          const uint32_t* cand, uint32_t cand_cap) {
+                          const uint32_t* cand, uint32_t cand_cap, int delta) {
   if (g.n == 0 || ql.nwaves == 0) return hipSuccess;
   constexpr size_t LDS_MAX = 160 * 1024;
   const size_t pre_bytes = ((size_t)ql.nwaves + 1) * 4;
@@ -3902,18 +3928,22 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   static const int fs_wg = diag_env("KM_FS_WG", 1);  // workgroups per CU (3: no measurable change)
   if (ch == 0)
     hipLaunchKernelGGL((k_fullscan<2, true>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
-                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, sse, gate);
+                       queue, qcount, ql, labels, ch, delta ? stats : (double*)nullptr, use_chain, pair_chain, sse, gate,
+                       delta);
   else if (G == 4)
     hipLaunchKernelGGL((k_fullscan<4, false>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
-                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, sse, gate);
+                       queue, qcount, ql, labels, ch, delta ? stats : (double*)nullptr, use_chain, pair_chain, sse, gate,
+                       delta);
   else
     hipLaunchKernelGGL((k_fullscan<2, false>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
-                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, sse, gate);
+                       queue, qcount, ql, labels, ch, delta ? stats : (double*)nullptr, use_chain, pair_chain, sse, gate,
+                       delta);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t tab_bytes = (size_t)(g.d + 1) * g.kp * 8;
   const size_t pres = (stats ? 2 : 1) * pre_bytes;
-  const int tab_kp = (stats && tab_bytes + pres <= LDS_MAX) ? g.kp : 0;
+  // (delta: direct atomics for the few rows that change clusters)
+  const int tab_kp = (stats && !delta && tab_bytes + pres <= LDS_MAX) ? g.kp : 0;
   // workgroups of the re-rank, in percent of n_cu (KM_RERANK_PCT).  Each
   // flushes its [k][d+1] table with global atomics, but fewer workgroups lose
   // more in parallelism than they save (c3 resolve 0.32-0.35 ms at 100%,
@@ -3922,10 +3952,10 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   const int rwg = std::max(1, n_cu * std::max(1, rpct) / 100);
   if (g.d > 256)
     hipLaunchKernelGGL(k_rerank2<true>, dim3(rwg), dim3(512), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
-                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap);
+                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap, delta);
   else
     hipLaunchKernelGGL(k_rerank2<false>, dim3(rwg), dim3(1024), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
-                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap);
+                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap, delta);
   return hipGetLastError();
 }
 

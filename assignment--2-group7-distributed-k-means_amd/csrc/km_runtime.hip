@@ -85,6 +85,24 @@ struct km_ctx {
   int screen = km::KM_SCREEN_X3_REFINE;
   bool fast_blocked = false;
   int screen_forced = -1;  // km_set_screen: a fixed mode, or -1 (the policy above)
+  // one-MFMA screen with in-kernel re-scoring (km_screen1.hip, KM_SCREEN_S1)
+  // and delta statistics: where the geometry has an instance, every assign
+  // runs k_s1 except the first after new data / centroids / a predict, which
+  // runs k_fused16 with full statistics; from then on the stats buffer
+  // carries only the moves of rows between clusters, and the update folds
+  // them into stats_full (km::launch_s1_apply) before it reads the sums.
+  // The choice depends only on the call sequence, never on a rank's data, so
+  // every rank of a job takes the same one.
+  bool s1 = false;
+  bool s1_recolor = true;        // colour the chains at the next prep
+  int32_t* s1_perm = nullptr;    // table index -> centroid
+  float* s1_cft = nullptr;       // fp32 centroids by table index (LDS copy)
+  float* s1_cn2o = nullptr;      // s^2 ||c||^2, MFMA output order
+  uint4* s1_img = nullptr;       // fragment-linear fp16 image of -2 s c
+  float* s1_cst = nullptr;       // bound constants
+  double* stats_full = nullptr;  // the full sums the deltas apply to
+  bool delta_ready = false;      // labels and stats_full describe one assignment
+  int stats_pending = 0;         // the last assign left 0 nothing, 1 full sums, 2 deltas in stats
   float* bal = nullptr;  // fast screen: image error maxima (2 floats)
   // statistics already zero (the batch update cleared them): no memset
   bool stats_clean = false;
@@ -256,6 +274,15 @@ void free_centroids(km_ctx* c) {
   dfree(c->cmax);
   dfree(c->cabs);
   dfree(c->stats_own);
+  dfree(c->s1_perm);
+  dfree(c->s1_cft);
+  dfree(c->s1_cn2o);
+  dfree(c->s1_img);
+  dfree(c->s1_cst);
+  dfree(c->stats_full);
+  c->s1 = false;
+  c->delta_ready = false;
+  c->stats_pending = 0;
   dfree(c->work);
   dfree(c->counts_dev);
   dfree(c->status_dev);
@@ -294,6 +321,7 @@ void free_data(km_ctx* c) {
   dfree(c->rows_scratch);
   c->scratch_rows = 0;
   c->loaded = false;
+  c->delta_ready = false;
 }
 
 // derived images (fp32 copy, transposed f64, fp16 hi/lo split, norms, bound
@@ -310,6 +338,14 @@ int prep(km_ctx* c, const double* src) {
                                    c->stream));
   KM_HIP(km::launch_prep_split(c->C32, c->g, c->cn2, c->xabs, c->cabs, c->Chi, c->Clo, c->cn2s, c->gate, c->stream));
   KM_HIP(km::launch_bound_consts(c->cmax, c->xabs, c->cabs, c->g, c->bnd, c->gate, c->stream));
+  if (c->s1) {
+    if (c->s1_recolor) {
+      KM_HIP(km::launch_s1_color(c->C32, c->g, c->s1_perm, c->gate, c->stream));
+      c->s1_recolor = false;
+    }
+    KM_HIP(km::launch_s1_prep(src, c->C32, c->g, c->s1_perm, c->cmax, c->xabs, c->cabs, c->s1_cft, c->s1_cn2o,
+                              c->s1_img, c->s1_cst, c->gate, c->stream));
+  }
   return KM_OK;
 }
 
@@ -391,6 +427,29 @@ bool fold_ok(km_ctx* c) {
 
 int run_assign(km_ctx* c, bool with_stats);
 
+// k_s1 for this assign: labels only (predict), or delta statistics once the
+// labels and the full sums of a previous iteration are in place (no SSE: its
+// residuals need every row, KM_SCREEN_S1 keeps the full-statistics screen)
+bool use_s1(km_ctx* c, bool with_stats) {
+  if (!c->s1) return false;
+  if (c->screen_forced >= 0 && c->screen_forced != KM_SCREEN_S1) return false;
+  return !with_stats || (c->delta_ready && !c->want_sse);
+}
+
+// before an update reads the statistics: delta -> fold into the full sums;
+// full -> keep them as the base of the next deltas
+int apply_stats(km_ctx* c) {
+  const int kind = c->stats_pending;
+  c->stats_pending = 0;
+  if (!c->s1) return KM_OK;
+  const bool keep = kind == 2 || (kind == 1 && !c->want_sse);
+  if (keep)
+    KM_HIP(km::launch_s1_apply(c->stats, c->stats_full, (int64_t)stats_len(c->g), kind == 2 ? 1 : 0, c->gate,
+                               c->stream));
+  c->delta_ready = keep;
+  return KM_OK;
+}
+
 // a deferred km_assign_stats launched on its own (any call but km_update_async
 // that follows it)
 int flush_assign(km_ctx* c) {
@@ -414,6 +473,26 @@ int run_assign(km_ctx* c, bool with_stats) {
     ProfScope ps(c, KM_K_ASSIGN, true);
     KM_HIP(km::launch_assign_small(c->X, g, c->C32, c->C64_cur, c->cmax, c->labels, c->stats, with_stats ? 1 : 0,
                                    sse ? 1 : 0, c->n_cu, c->gate, c->stream, small_tail(c)));
+    return KM_OK;
+  }
+  c->stats_pending = with_stats ? 1 : 0;
+  if (c->fused && use_s1(c, with_stats)) {
+    {
+      ProfScope ps(c, KM_K_ASSIGN, true);
+      KM_HIP(km::launch_s1(c->X, c->xnorm, g, c->s1_img, c->s1_cn2o, c->s1_cft, c->s1_perm, c->s1_cst,
+                           c->labels, c->queue, c->qcount, with_stats ? c->stats : nullptr, with_stats ? 1 : 0,
+                           c->n_cu, &c->ql, c->gate, c->stream));
+    }
+    {
+      // the queued rows: near-ties of the re-scored candidates and the rows
+      // the chain certificate leaves open, resolved in float64 (delta: they
+      // still hold their previous labels)
+      ProfScope ps(c, KM_K_RESOLVE);
+      KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels,
+                                with_stats ? c->stats : nullptr, c->n_cu, c->gate, c->stream, nullptr, nullptr, 0,
+                                with_stats ? 1 : 0));
+    }
+    c->stats_pending = with_stats ? 2 : 0;
     return KM_OK;
   }
   if (c->fused) {
@@ -551,6 +630,11 @@ int km_destroy(km_ctx* c) {
 int km_set_stream(km_ctx* c, void* s) {
   KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
   KM_HIP(hipSetDevice(c->device));
+  {
+    // a deferred assign runs on the stream it was enqueued for
+    const int rcf = flush_assign(c);
+    if (rcf != KM_OK) return rcf;
+  }
   KM_HIP(hipStreamSynchronize(c->stream));
   c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
   return KM_OK;
@@ -589,6 +673,11 @@ int km_load_begin(km_ctx* c, int64_t n, int32_t d) {
   KM_REQUIRE(n >= 0 && n < (int64_t)UINT32_MAX, KM_ERR_ARG, "km_load_begin: n out of range");
   KM_REQUIRE(d > 0, KM_ERR_ARG, "km_load_begin: d must be positive");
   KM_HIP(hipSetDevice(c->device));
+  {
+    // a deferred assign reads the rows being replaced (flush first)
+    const int rcf = flush_assign(c);
+    if (rcf != KM_OK) return rcf;
+  }
   KM_HIP(hipStreamSynchronize(c->stream));
   free_data(c);
   free_centroids(c);
@@ -619,6 +708,11 @@ int km_load_rows(km_ctx* c, int64_t row0, const float* rows, int64_t nrows) {
   if (nrows == 0) return KM_OK;
   KM_REQUIRE(rows, KM_ERR_ARG, "km_load_rows: null rows");
   KM_HIP(hipSetDevice(c->device));
+  {
+    const int rcf = flush_assign(c);  // it must read the rows it was called for
+    if (rcf != KM_OK) return rcf;
+  }
+  c->delta_ready = false;  // the rows behind the labels change
   const int d = c->g.d, dp = c->g.dp;
   // double-buffered pinned staging: the host fills one half while the DMA
   // of the other is in flight (one event per half, one sync at the end)
@@ -675,26 +769,31 @@ int km_sum_x(km_ctx* c, double* out) {
 
 int km_set_screen(km_ctx* c, int32_t mode) {
   KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
-  KM_REQUIRE(mode >= -1 && mode <= km::KM_SCREEN_FAST2, KM_ERR_ARG, "km_set_screen: mode must be -1..3");
+  KM_REQUIRE(mode >= -1 && mode <= KM_SCREEN_S1, KM_ERR_ARG, "km_set_screen: mode must be -1..4");
 #ifndef KM_DIAG
   // the fast screens (k_fused1) lost end to end on every BASELINE shape
   // (DESIGN.md "Fast screen"): built in the diagnostic library only
-  KM_REQUIRE(mode <= km::KM_SCREEN_X3_REFINE, KM_ERR_UNSUPPORTED,
+  KM_REQUIRE(mode <= km::KM_SCREEN_X3_REFINE || mode == KM_SCREEN_S1, KM_ERR_UNSUPPORTED,
              "km_set_screen: fast screens (modes 2, 3) are in the diagnostic build only");
 #endif
   c->screen_forced = mode;
-  if (mode >= 0) c->screen = mode;
+  if (mode >= 0 && mode != KM_SCREEN_S1) c->screen = mode;
   return KM_OK;
 }
 
 int km_get_screen(km_ctx* c, int32_t* mode) {
   KM_REQUIRE(c && mode, KM_ERR_ARG, "null ctx");
-  *mode = c->screen;
+  // the screen of the next fused assign with statistics
+  *mode = (c->fused && use_s1(c, true)) ? KM_SCREEN_S1 : c->screen;
   return KM_OK;
 }
 
 int km_set_sse(km_ctx* c, int32_t enable) {
   KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
+  {
+    const int rcf = flush_assign(c);  // launched with the residual choice it was called under
+    if (rcf != KM_OK) return rcf;
+  }
   c->want_sse = enable != 0;
   return KM_OK;
 }
@@ -754,7 +853,20 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
     else
       c->path = 0;
     c->fused = (c->path == 2) && km::fused_path_ok(c->g) && !fused_disabled();
+    c->s1 = c->fused && km::fused16_ok(c->g) && km::s1_ok(c->g) && km::diag_env("KM_S1", 1) != 0;
+    if (c->s1) {
+      const size_t nt = km::s1_table_entries(c->g);
+      KM_HIP(hipMalloc(&c->s1_perm, sizeof(int32_t) * nt));
+      KM_HIP(hipMalloc(&c->s1_cft, sizeof(float) * nt * (dp + 4)));
+      KM_HIP(hipMalloc(&c->s1_cn2o, sizeof(float) * kp));
+      KM_HIP(hipMalloc(&c->s1_img, sizeof(_Float16) * kp * dp));
+      KM_HIP(hipMalloc(&c->s1_cst, sizeof(float) * 8));
+      KM_HIP(hipMalloc(&c->stats_full, sizeof(double) * stats_len(c->g)));
+    }
   }
+  c->s1_recolor = true;
+  c->delta_ready = false;
+  c->stats_pending = 0;
   KM_HIP(hipMemcpyAsync(c->C64_cur, C, sizeof(double) * k * d, hipMemcpyHostToDevice, c->stream));
   int rc = prep(c);
   if (rc != KM_OK) return rc;
@@ -853,6 +965,10 @@ int km_update(km_ctx* c, km_status* st, int64_t* counts) {
     if (rcf != KM_OK) return rcf;
   }
   {
+    const int rca = apply_stats(c);
+    if (rca != KM_OK) return rca;
+  }
+  {
     ProfScope ps(c, KM_K_UPDATE);
     KM_HIP(km::launch_update(c->stats, c->C64_cur, c->g, c->C64_new, c->work, c->counts_dev, c->qcount,
                              c->ql.nwaves, c->status_dev, c->gate, -1.0, 0, c->stream));
@@ -887,6 +1003,11 @@ int km_set_layout(km_ctx* c, const int64_t* sizes, int32_t nparts, int64_t row0,
   KM_REQUIRE(c && c->loaded, KM_ERR_STATE, "km_set_layout: load data first");
   KM_REQUIRE(nparts >= 0 && (nparts == 0 || sizes), KM_ERR_ARG, "km_set_layout: bad partitions");
   KM_HIP(hipSetDevice(c->device));
+  {
+    // a deferred assign was decided under the old repair arming (fold_ok)
+    const int rcf = flush_assign(c);
+    if (rcf != KM_OK) return rcf;
+  }
   KM_HIP(hipStreamSynchronize(c->stream));
   free_repair(c);
   dfree(c->rep_sizes);
@@ -927,6 +1048,12 @@ int km_batch_begin(km_ctx* c) {
   KM_REQUIRE(!c->in_batch, KM_ERR_STATE, "km_batch_begin: a batch is open");
   KM_HIP(hipSetDevice(c->device));
   KM_HIP(hipMemsetAsync(c->gate, 0, sizeof(int), c->stream));
+  if (c->s1) {
+    // the chain colouring follows the centroids once per batch (a stale one
+    // only queues rows: the certificate uses R_c of the current centroids)
+    c->s1_recolor = true;
+    if (c->prep_of == c->C64_cur) c->prep_of = nullptr;
+  }
   c->in_batch = true;
   c->batch_n = 0;
   ++c->batch_seq;
@@ -947,6 +1074,13 @@ int km_update_async(km_ctx* c, double tol, int64_t empty_seed) {
   // no repair behind it, writes the next assign's centroid images itself
   const bool one = km::update_one_ok(c->g);
   const bool fold_prep = one && c->path == 1 && !repair;
+  if (c->assign_pending && !fold_ok(c)) {
+    // the fold was decided at km_assign_stats; if its conditions no longer
+    // hold (a stats buffer bound or exported since, the repair re-armed),
+    // the assign runs on its own and the update below is the usual launch
+    const int rcf = flush_assign(c);
+    if (rcf != KM_OK) return rcf;
+  }
   if (c->assign_pending) {
     // one launch: assign + sums + queued rows + update (last workgroup)
     c->assign_pending = false;
@@ -970,6 +1104,10 @@ int km_update_async(km_ctx* c, double tol, int64_t empty_seed) {
     }
     c->stats_clean = true;  // the update cleared them
     return finish_update(c, slot, fold_prep);
+  }
+  {
+    const int rca = apply_stats(c);
+    if (rca != KM_OK) return rca;
   }
   {
     ProfScope ps(c, KM_K_UPDATE);
@@ -1255,6 +1393,7 @@ int km_predict(km_ctx* c, int32_t* labels_out) {
   }
   int rc = run_assign(c, false);
   if (rc != KM_OK) return rc;
+  c->delta_ready = false;  // the labels are now predict's, not the sums' assignment
   if (labels_out && c->g.n > 0)
     KM_HIP(hipMemcpyAsync(labels_out, c->labels, sizeof(int32_t) * c->g.n, hipMemcpyDeviceToHost, c->stream));
   KM_HIP(hipStreamSynchronize(c->stream));

@@ -1,0 +1,711 @@
+// One-MFMA screen with in-kernel exact re-scoring (the c3 class: kp * dp <=
+// 16384, dp a multiple of 32).  DESIGN.md section 2, "One-MFMA screen".
+//
+// Reference: kmeans_spark.py:147-159 (assign_partition: np.argmin of
+// np.linalg.norm(C - x, axis=1)) and :169-173 (reduceByKey of (x, 1)).
+//
+// Why a new kernel: the fp16x3 screen (k_fused16) issues three f16 MFMAs per
+// product and holds its 256-register images at one wave per SIMD; its tile
+// body (split, merges, sums) cannot overlap the MFMAs, and the chip holds its
+// clock down under the MFMA density.  Here:
+//   * one v_mfma_f32_16x16x32_f16 per product: image RN16(-2 s c) (32 KB of
+//     LDS at c3, read as A fragments one block pair ahead) times the row
+//     RN16(s x).  Its error is large (E ~ 5 in squared distance units at c3),
+//     so the screen only proposes candidates;
+//   * every row whose screen cannot settle it (about 12% at c3) has its
+//     candidates re-scored exactly in fp32 direct form ||x - c'||^2 from an
+//     LDS copy of the fp32 centroids, with a rigorous error bound; only
+//     near-ties of the candidates (1e-6 relative) go to the float64 resolvers;
+//   * 16-row tiles, two waves per SIMD (512-thread workgroups), rows
+//     double-buffered in registers: one wave's VALU work hides under the
+//     other's MFMAs and loads;
+//   * statistics: either none (predict) or DELTAS -- a row whose label did not
+//     change since the last iteration adds nothing; a changed row moves its
+//     x from the old cluster's float64 sums to the new one's (global float64
+//     atomics).  The runtime keeps the full sums (km_runtime.hip, "delta
+//     statistics"), so the sums the update reads are the reference's
+//     reduceByKey sums over every row, exactly as a fresh pass would produce
+//     them up to float64 summation order.
+//
+// Candidate certificate (all bounds rigorous, real arithmetic on the float64
+// centroids c; c' = fp32 image):
+//   * chains: the output layout gives each lane 8 accumulator positions per
+//     block of 32 centroids; position (cb, i) over the NB blocks is a chain
+//     (32 chains per row, NB members).  Each lane keeps the chain's best two
+//     keys (v_min3 / v_med3 over block pairs, 5 VALU per two keys, the block
+//     id in the low mantissa bits of every key).
+//   * a greedy colouring (k_s1_color) puts mutually distant centroids in one
+//     chain, so that two members of a chain are rarely both close to a row.
+//   * keys K~ = s^2(||c||^2 - 2 c.x) + e, |e| <= E(x) (k_s1_prep's bound).
+//     m = the smallest head; every centroid whose key exceeds m + 2E (+ the
+//     packing perturbation) is strictly farther than the argmin.  The heads
+//     below that threshold T are the candidates; a chain whose second key is
+//     below T too (a member that is neither head nor excluded) sends the row
+//     to the full float64 scan.
+//   * one candidate: it is the argmin.  Otherwise each candidate is
+//     re-scored, D~ = fp32 sum of (x - c')^2, |D~ - D'| <= 36u D', and
+//     ||x - c|| in [sqrt(D'(1-48u)) - g, sqrt(D'(1+48u)) + g], g = u cmax.
+//     The winner must beat every other candidate's lower bound strictly;
+//     otherwise the row is queued (kind 1: the two candidates re-ranked in
+//     float64 by k_rerank2; kind 2: full float64 scan by k_fullscan).
+#include <float.h>
+
+#include "km_internal.h"
+
+namespace km {
+
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr float U24 = 5.9604644775390625e-08f;  // 2^-24
+constexpr float U16 = 4.8828125e-04f;           // 2^-11, fp16 unit roundoff
+constexpr int S1_WAVES = 8;                     // 512 threads: two waves per SIMD
+constexpr int S1_LMAX = 4;                      // candidates re-scored per row
+
+constexpr int ceil_log2_c(int v) { return v <= 1 ? 0 : 1 + ceil_log2_c((v + 1) / 2); }
+
+__device__ __forceinline__ uint32_t f2u(float v) { return __float_as_uint(v); }
+__device__ __forceinline__ float u2f(uint32_t v) { return __uint_as_float(v); }
+
+// the four quarter lanes of a row (l, l ^ 16, l ^ 32, l ^ 48): min / sum
+__device__ __forceinline__ float quad_min(float v) {
+  auto p = __builtin_amdgcn_permlane16_swap(f2u(v), f2u(v), false, false);
+  v = __builtin_fminf(u2f(p[0]), u2f(p[1]));
+  p = __builtin_amdgcn_permlane32_swap(f2u(v), f2u(v), false, false);
+  return __builtin_fminf(u2f(p[0]), u2f(p[1]));
+}
+// the same order of additions in all four lanes ((l0 + l16) + (l32 + l48)):
+// every lane of the row holds the bit-identical sum
+__device__ __forceinline__ float quad_sum(float v) {
+  auto p = __builtin_amdgcn_permlane16_swap(f2u(v), f2u(v), false, false);
+  v = u2f(p[0]) + u2f(p[1]);
+  p = __builtin_amdgcn_permlane32_swap(f2u(v), f2u(v), false, false);
+  return u2f(p[0]) + u2f(p[1]);
+}
+__device__ __forceinline__ int32_t quad_min_i(int32_t v) {
+  auto p = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+  v = min((int32_t)p[0], (int32_t)p[1]);
+  p = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
+  return min((int32_t)p[0], (int32_t)p[1]);
+}
+// float bits -> int32 with the same order (distinct bits stay distinct, -0 < +0);
+// its own inverse
+__device__ __forceinline__ int32_t mono(uint32_t b) { return (int32_t)(b ^ ((uint32_t)((int32_t)b >> 31) >> 1)); }
+__device__ __forceinline__ uint32_t unmono(int32_t v) { return (uint32_t)v ^ ((uint32_t)(v >> 31) >> 1); }
+__device__ __forceinline__ uint32_t quad_add_u(uint32_t v) {
+  auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = p[0] + p[1];
+  p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return p[0] + p[1];
+}
+
+__device__ __forceinline__ float s1_scale(float xabs, float cabs) {
+  // power-of-two scale: max(|x|, |c|) * s < 2^14 (km_kernels.hip mfma_scale)
+  const float m = fmaxf(xabs, cabs);
+  if (!(m > 0.0f) || !(m < 3.0e38f)) return 1.0f;
+  int e;
+  (void)frexpf(m, &e);
+  return ldexpf(1.0f, 14 - e);
+}
+
+}  // namespace
+
+// table index of chain c, member b: (c << MB) | b
+struct S1Geo {
+  int nb, mb, ns2;
+};
+
+// ---------------------------------------------------------------------------
+// Greedy colouring of the centroids into 32 chains of nb members (one
+// workgroup).  In index order, centroid j joins the non-full chain whose
+// members are farthest from it (largest minimum distance; ties: lowest
+// chain).  perm[(chain << mb) | member] = centroid, -1 for pads.  Only a
+// cost choice: the certificate uses R_c computed for whatever colouring is
+// current, so a stale or poor colouring can queue rows, never mislabel them.
+// ---------------------------------------------------------------------------
+template <int DPC>
+__global__ __launch_bounds__(512) void k_s1_color(const float* __restrict__ C32, int k, int dp, int nb, int mb,
+                                                  int32_t* __restrict__ perm, const int* __restrict__ gate) {
+  if (*gate) return;
+  __shared__ unsigned int cmin[32];
+  __shared__ int cnt[32];
+  __shared__ int cls[512];
+  const int t = threadIdx.x;
+  float cv[DPC];
+#pragma unroll
+  for (int f = 0; f < DPC; ++f) cv[f] = (t < k && f < dp) ? C32[(size_t)t * dp + f] : 0.0f;
+  if (t < 32) cnt[t] = 0;
+  cls[t] = -1;
+  __syncthreads();
+  for (int j = 0; j < k; ++j) {
+    if (t < 32) cmin[t] = 0x7F800000u;  // +inf
+    __syncthreads();
+    if (t < j) {
+      float s = 0.0f;
+#pragma unroll
+      for (int f = 0; f < DPC; ++f) {
+        const float df = cv[f] - C32[(size_t)j * dp + f];
+        s = fmaf(df, df, s);
+      }
+      atomicMin(&cmin[cls[t]], __float_as_uint(s));
+    }
+    __syncthreads();
+    if (t < 64) {
+      // (eligible, distance bits, lowest chain) maximum over the 32 chains
+      uint64_t key = 0;
+      if (t < 32 && cnt[t] < nb) key = ((uint64_t)(cmin[t] + 1u) << 8) | (uint64_t)(31 - t);
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const uint64_t other = __shfl_xor(key, o);
+        key = other > key ? other : key;
+      }
+      if (t == 0) {
+        const int c = 31 - (int)(key & 255u);
+        const int m = cnt[c];
+        cls[j] = c;
+        cnt[c] = m + 1;
+        perm[(c << mb) | m] = j;
+      }
+    }
+    __syncthreads();
+  }
+  // pads: members cnt[c] .. (1 << mb) - 1 of every chain
+  for (int i = t; i < (32 << mb); i += blockDim.x) {
+    const int c = i >> mb, m = i & ((1 << mb) - 1);
+    if (m >= cnt[c]) perm[i] = -1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Per-iteration images of the current centroids in the colouring's order.
+// Blocks 0 .. (32 << mb) - 1: table index ti = (chain << mb) | member:
+//   cft[ti][f]  fp32 centroid (row stride dp + 4: the LDS copy's bank spread)
+//   cn2o[p]     s^2 ||c||^2 (float64 norm, rounded once; pads 1e30) at the
+//               MFMA output position p = 32 member + 16 (chain >> 4) + (chain & 15)
+//   img         fragment-linear A operands RN16(-2 s c') of v_mfma_f32_16x16x32_f16:
+//               fragment (member, cb, t), lane l = 16 q + M holds centroid
+//               chain 16 cb + M, features fq q + 8 t .. + 8 (fq = dp / 4)
+// Last block: bound constants.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_s1_prep(const double* __restrict__ C64, const float* __restrict__ C32, int k,
+                                                int d, int dp, S1Geo sg, const int32_t* __restrict__ perm,
+                                                const float* __restrict__ cmax, const float* __restrict__ xabs,
+                                                const float* __restrict__ cabs, float* __restrict__ cft,
+                                                float* __restrict__ cn2o, uint4* __restrict__ img,
+                                                float* __restrict__ cst,
+                                                const int* __restrict__ gate) {
+  if (*gate) return;
+  const int b = blockIdx.x, th = threadIdx.x;
+  const int nt = 32 << sg.mb;
+  const float s = s1_scale(*xabs, *cabs);
+  const int cs = dp + 4;
+  if (b < nt) {
+    const int chain = b >> sg.mb, member = b & ((1 << sg.mb) - 1);
+    const int j = member < sg.nb ? perm[b] : -1;
+    for (int f = th; f < cs; f += 64) cft[(size_t)b * cs + f] = (j >= 0 && f < d) ? C32[(size_t)j * dp + f] : 0.0f;
+    if (member >= sg.nb) return;
+    const int cb = chain >> 4, M = chain & 15;
+    if (th == 0) {
+      double nn = 0.0;
+      if (j >= 0)
+        for (int f = 0; f < d; ++f) nn = fma(C64[(size_t)j * d + f], C64[(size_t)j * d + f], nn);
+      cn2o[32 * member + 16 * cb + M] = j >= 0 ? (float)(nn * (double)s * (double)s) : 1e30f;
+    }
+    const int fq = dp / 4;
+    if (th < 4 * sg.ns2) {
+      const int q = th / sg.ns2, t = th - q * sg.ns2;
+      f16x8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int f = fq * q + 8 * t + e;
+        v[e] = (j >= 0 && f < d) ? (_Float16)(-2.0f * s * C32[(size_t)j * dp + f]) : (_Float16)0.0f;
+      }
+      img[((size_t)(member * 2 + cb) * sg.ns2 + t) * 64 + 16 * q + M] = __builtin_bit_cast(uint4, v);
+    }
+    return;
+  }
+  if (th == 0) {
+    // screen error bound E = e1 ||x|| + e0 in scaled units (||x|| unscaled),
+    // see the header and DESIGN.md "One-MFMA screen": image and row rounding
+    // (fp16, the image of the fp32 c' whose own rounding adds u), the fp32
+    // rounding of s^2 ||c||^2, the 16x16x32 accumulation model (per MFMA 4
+    // roundings of a partial sum and 28 u of the largest product; ns2 MFMAs
+    // per key), fp16 underflow; times 1.25
+    const float cm = *cmax, ca = *cabs * (1.0f + U24), xa = *xabs;
+    const float s2 = s * s, sq = sqrtf((float)dp) * 1.0001f, nm = (float)sg.ns2;
+    const float e1 = 1.25f * (2.0f * s2 * cm * (2.0f * U16 + U16 * U16 + 2.0f * U24) +
+                              nm * 4.0f * U24 * 2.0f * s2 * cm * (1.0f + 2.0f * U16) +
+                              ldexpf(1.0f, -25) * s * sq * (1.0f + U16));
+    const float e0 = 1.25f * (U24 * s2 * cm * cm + nm * (4.0f * U24 * s2 * cm * cm +
+                                                          28.0f * U24 * 2.0f * s2 * ca * xa * (1.0f + U16) * (1.0f + U16)) +
+                              ldexpf(1.0f, -24) * s * sq * cm);
+    cst[0] = s;
+    cst[1] = e1 * 1.0001f;
+    cst[2] = e0 * 1.0001f + 1e-30f;
+    cst[3] = U24 * cm * 1.01f + 1e-37f;  // g: ||c - c'|| <= u ||c||
+  }
+}
+
+struct S1Args {
+  const float* X;
+  const float* xnorm;  // per-row upper bound of ||x|| (unscaled)
+  int64_t n;
+  int k, d;
+  uint32_t seg;
+  const uint4* img;
+  const float* cn2o;
+  const float* cft;
+  const int32_t* perm;
+  const float* cst;
+  int32_t* labels;
+  QEntry* queue;
+  uint32_t* qcount;
+  double* stats;  // DELTA: [k][d+1] float64 deltas (sums, counts)
+  const int* gate;
+};
+
+// MODE 0: labels only (predict; every decided row's label written, queued
+// rows' by the resolvers).  MODE 1: delta statistics (the previous labels are
+// read; only changed labels are written and moved in the sums; queued rows
+// keep their previous label for the resolvers to compare).
+template <int NS2, int NB, int MODE>
+__global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
+  if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
+  constexpr int DP = 32 * NS2;
+  constexpr int FQ = 8 * NS2;  // features per quarter lane
+  constexpr int KP = 32 * NB;
+  constexpr int MB = ceil_log2_c(NB);
+  constexpr int NT = 32 << MB;      // table entries
+  constexpr int CS = DP + 4;        // LDS row stride of the fp32 centroids (floats)
+  constexpr uint32_t SLOTM = (uint32_t)NT - 1u;
+  constexpr uint32_t KMASK = ~SLOTM;
+  // key packing perturbation: the low 5 + MB mantissa bits replaced
+  constexpr float RHO = (float)SLOTM * 1.1920928955078125e-07f * 1.0001f;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint4* sImg = reinterpret_cast<const uint4*>(smem);    // [NB][2][NS2][64] A fragments
+  float* sCf = reinterpret_cast<float*>(smem + KP * DP * 2);  // [NT][CS]
+  float* sCn = sCf + NT * CS;                                 // [KP] output order
+  int32_t* sPerm = reinterpret_cast<int32_t*>(sCn + KP);      // [NT]
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int c16 = lane & 15;
+  const int q = lane >> 4;
+  {
+    uint4* di = reinterpret_cast<uint4*>(smem);
+    for (int i = threadIdx.x; i < KP * DP / 8; i += S1_WAVES * 64) di[i] = A.img[i];
+    const float4* src = reinterpret_cast<const float4*>(A.cft);
+    float4* dst = reinterpret_cast<float4*>(sCf);
+    for (int i = threadIdx.x; i < NT * CS / 4; i += S1_WAVES * 64) dst[i] = src[i];
+    for (int i = threadIdx.x; i < KP; i += S1_WAVES * 64) sCn[i] = A.cn2o[i];
+    for (int i = threadIdx.x; i < NT; i += S1_WAVES * 64) sPerm[i] = A.perm[i];
+  }
+  __syncthreads();
+
+  const float s = A.cst[0], e1 = A.cst[1], e0 = A.cst[2], gam = A.cst[3];
+  // rows fit 32 bits (km_load_begin: n < 2^32 - 1): 32-bit row and tile arithmetic
+  const uint32_t n = (uint32_t)A.n;
+  const uint32_t ntiles = (n + 15u) / 16u;
+  const uint32_t gw = blockIdx.x * S1_WAVES + wave;
+  const uint32_t nw = gridDim.x * S1_WAVES;
+  QEntry* wq = A.queue + (size_t)gw * A.seg;
+  uint32_t qn = 0, qf = 0;
+  const int d = A.d;
+  // chain id bits of this lane's 8 accumulator positions (cb, i): chain 16 cb + 4 q + i
+  const uint32_t qbits = (uint32_t)(4 * q) << MB;
+
+  struct Buf {
+    float4 x[FQ / 4];
+    float xn;
+    int32_t old;
+  };
+  auto load = [&](uint32_t tile, Buf& B) {
+    const uint32_t row = tile * 16u + (uint32_t)c16;
+    const uint32_t rr = row < n ? row : (n - 1u);
+    const float4* xr = reinterpret_cast<const float4*>(A.X + (size_t)rr * DP + FQ * q);
+#pragma unroll
+    for (int u = 0; u < FQ / 4; ++u) B.x[u] = xr[u];
+    B.xn = A.xnorm[rr];
+    if constexpr (MODE == 1) B.old = A.labels[rr];
+  };
+
+  auto process = [&](uint32_t tile, const Buf& B) {
+    const uint32_t row = tile * 16u + (uint32_t)c16;
+    const bool valid = row < n;
+    // B operands: RN16(s x), features FQ q + 8 t .. + 8 of slice t
+    f16x8 bx[NS2];
+#pragma unroll
+    for (int t = 0; t < NS2; ++t) {
+      const float4 a = B.x[2 * t], c = B.x[2 * t + 1];
+      bx[t][0] = (_Float16)(a.x * s);
+      bx[t][1] = (_Float16)(a.y * s);
+      bx[t][2] = (_Float16)(a.z * s);
+      bx[t][3] = (_Float16)(a.w * s);
+      bx[t][4] = (_Float16)(c.x * s);
+      bx[t][5] = (_Float16)(c.y * s);
+      bx[t][6] = (_Float16)(c.z * s);
+      bx[t][7] = (_Float16)(c.w * s);
+    }
+    // this lane's 8 chains: best key (head, member id in the low MB bits)
+    // and second key
+    float h[2][4], h2[2][4];
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h[cb][i] = h2[cb][i] = FLT_MAX;
+    const float4* cnl = reinterpret_cast<const float4*>(sCn + 4 * q);  // + 8 blk + 4 cb
+    // a block pair's operands from LDS: A fragments (lane-linear 1 KiB
+    // pieces, conflict-free) and accumulator inits; the next pair's are
+    // read while this pair's MFMAs and key updates run
+    struct Pair {
+      f16x8 a[2][2][NS2];  // [block of the pair][cb][t]
+      float4 c[2][2];      // [block of the pair][cb]
+    };
+    auto load_pair = [&](int blk, Pair& P) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          P.c[e][cb] = cnl[8 * (blk + e) + 4 * cb];
+#pragma unroll
+          for (int t = 0; t < NS2; ++t)
+            P.a[e][cb][t] = __builtin_bit_cast(f16x8, sImg[(((blk + e) * 2 + cb) * NS2 + t) * 64 + lane]);
+        }
+    };
+    Pair pr[2];
+    load_pair(0, pr[0]);
+    // blocks in pairs: two members per step, new best = min3(best, ka, kb),
+    // new second = min(second, med3(best, ka, kb))
+#pragma unroll
+    for (int blk = 0; blk < NB; blk += 2) {
+      const Pair& P = pr[(blk >> 1) & 1];
+      if (blk + 2 < NB) load_pair(blk + 2, pr[((blk >> 1) + 1) & 1]);
+      f32x4 a0[2], a1[2];
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        a0[cb] = f32x4{P.c[0][cb].x, P.c[0][cb].y, P.c[0][cb].z, P.c[0][cb].w};
+        a1[cb] = f32x4{P.c[1][cb].x, P.c[1][cb].y, P.c[1][cb].z, P.c[1][cb].w};
+      }
+#pragma unroll
+      for (int t = 0; t < NS2; ++t)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          a0[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(P.a[0][cb][t], bx[t], a0[cb], 0, 0, 0);
+          a1[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(P.a[1][cb][t], bx[t], a1[cb], 0, 0, 0);
+        }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float ka = u2f((f2u(a0[cb][i]) & KMASK) | (uint32_t)blk);
+          const float kb = u2f((f2u(a1[cb][i]) & KMASK) | (uint32_t)(blk + 1));
+          const float t = __builtin_amdgcn_fmed3f(h[cb][i], ka, kb);
+          h[cb][i] = __builtin_fminf(__builtin_fminf(h[cb][i], ka), kb);
+          h2[cb][i] = __builtin_fminf(h2[cb][i], t);
+        }
+      // one block pair in flight (plus the next one's operands): the
+      // scheduler would otherwise hoist every pair's reads and MFMAs ahead of
+      // the key updates; the partner wave on the SIMD fills the MFMA pipe
+      // while this one updates its keys
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // full slot ids in the heads, (chain << MB) | member, as order-preserving
+    // integers: the candidate count and the rounds below compare distinct
+    // keys exactly, whatever the float mode does with tiny values
+    int32_t hk[2][4];
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hk[cb][i] = mono(f2u(h[cb][i]) | qbits | ((uint32_t)(16 * cb + i) << MB));
+
+    // smallest head of the row and the candidate threshold T
+    int32_t ml = hk[0][0];
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ml = min(ml, hk[cb][i]);
+    const int32_t mki = quad_min_i(ml);
+    const float m = u2f(unmono(mki));
+    const float xn = B.xn;
+    const float E = fmaf(e1, xn, e0);
+    const bool bad = !(m >= -3.0e38f && m <= 3.0e38f) || !(xn <= 3.0e38f);
+    constexpr float RP = RHO * (1.0f + 2.0f * RHO);
+    const float R = m + RP * fabsf(m) + 2.0f * E;
+    float T = R >= 0.0f ? R / (1.0f - RP) : R / (1.0f + RP);
+    T = T >= 0.0f ? T * (1.0f + 4.0f * U24) : T * (1.0f - 4.0f * U24);
+    const int32_t Tk = mono(f2u(T));
+    // candidates: heads <= T (low 16 bits of the quad sum); chains whose
+    // second key is <= T too (high 16 bits: the row goes to the full scan)
+    uint32_t cl = 0;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        cl += ((hk[cb][i] <= Tk) ? 1u : 0u) + ((mono(f2u(h2[cb][i])) <= Tk) ? 0x10000u : 0u);
+    const uint32_t cq = bad ? 0u : quad_add_u(cl);
+    const uint32_t cnt = cq & 0xFFFFu;
+    const bool ovf = (cq >> 16) != 0u;
+
+    // re-scored rows: the winner (smallest upper bound U1, its lower bound
+    // L1, slot s1) and the smallest lower bound of the other candidates (Lo,
+    // slot s2)
+    const uint32_t sm = unmono(mki) & SLOTM;
+    uint32_t s1 = sm, s2 = sm;
+    float U1 = FLT_MAX, L1 = FLT_MAX, Lo = FLT_MAX;
+    const bool need = valid && !bad && !ovf && cnt >= 2u && cnt <= (uint32_t)S1_LMAX;
+    if (__ballot(need) != 0ull) {
+      // candidates in ascending key order: round r takes the smallest head
+      // above the previous one; every lane of the wave re-scores (a row with
+      // no candidate left scores slot 0 and ignores it)
+      int32_t prev = INT32_MIN;
+#pragma unroll 1
+      for (int r = 0; r < S1_LMAX; ++r) {
+        const bool act = need && (uint32_t)r < cnt;
+        if (__ballot(act) == 0ull) break;
+        int32_t nl = INT32_MAX;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) nl = min(nl, hk[cb][i] > prev ? hk[cb][i] : INT32_MAX);
+        const int32_t cur = quad_min_i(nl);
+        prev = cur;
+        const uint32_t sl = act ? (unmono(cur) & SLOTM) : 0u;
+        const float4* cp = reinterpret_cast<const float4*>(sCf + sl * CS + FQ * q);
+        float acc = 0.0f;
+#pragma unroll
+        for (int u = 0; u < FQ / 4; ++u) {
+          const float4 c = cp[u];
+          const float4 x = B.x[u];
+          const float d0 = x.x - c.x, d1 = x.y - c.y, d2 = x.z - c.z, d3 = x.w - c.w;
+          acc = fmaf(d0, d0, acc);
+          acc = fmaf(d1, d1, acc);
+          acc = fmaf(d2, d2, acc);
+          acc = fmaf(d3, d3, acc);
+        }
+        const float Dt = quad_sum(acc);
+        // |Dt - D'| <= (FQ + 4) u D' <= 36 u D' (D' = ||x - c'||^2, FQ <= 32),
+        // then ||x - c|| = sqrt(D') +- g; sqrt and products: 8 u
+        const float U = (sqrtf(Dt * (1.0f + 48.0f * U24)) + gam) * (1.0f + 8.0f * U24);
+        const float L = (sqrtf(Dt * (1.0f - 48.0f * U24)) - gam) * (1.0f - 8.0f * U24);
+        // select form throughout (branchy running minima
+        // are miscompiled in divergent code on this toolchain)
+        const bool w = act && U < U1;              // new winner
+        const float Lc = w ? L1 : L;               // the displaced winner, or this one, joins the others
+        const uint32_t sc = w ? s1 : sl;
+        const bool lo = act && Lc < Lo;
+        Lo = lo ? Lc : Lo;
+        s2 = lo ? sc : s2;
+        U1 = w ? U : U1;
+        L1 = w ? L : L1;
+        s1 = w ? sl : s1;
+      }
+    }
+    // decision: 0 decided, 1 pair re-rank (k_rerank2), 2 full scan (k_fullscan)
+    const int32_t lab1 = sPerm[s1];
+    const int32_t lab2 = sPerm[s2];
+    uint32_t kind = 2u;
+    if (!bad && !ovf && cnt >= 1u && cnt <= (uint32_t)S1_LMAX && lab1 >= 0) {
+      if (cnt == 1u || Lo > U1)
+        kind = 0u;
+      else if (cnt == 2u && lab2 >= 0)
+        kind = 1u;
+    }
+    const bool decided = valid && kind == 0u;
+    if constexpr (MODE == 0) {
+      if (decided && q == 0) A.labels[row] = lab1;
+    } else {
+      // (a previous label is always a cluster index; clamped so that a
+      // corrupt one can never address outside the sums)
+      const int32_t old = (int32_t)min((uint32_t)B.old, (uint32_t)(A.k - 1));
+      const bool changed = decided && lab1 != old;
+      if (__ballot(changed) != 0ull && changed) {
+        if (q == 0) A.labels[row] = lab1;
+        double* so = A.stats + (size_t)old * (d + 1);
+        double* sn = A.stats + (size_t)lab1 * (d + 1);
+        if (d == DP) {
+          // no padding: one base per lane, the features at constant offsets
+          double* po = so + FQ * q;
+          double* pn = sn + FQ * q;
+#pragma unroll
+          for (int u = 0; u < FQ / 4; ++u) {
+            const float xv[4] = {B.x[u].x, B.x[u].y, B.x[u].z, B.x[u].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              atomicAdd(po + 4 * u + e, -(double)xv[e]);
+              atomicAdd(pn + 4 * u + e, (double)xv[e]);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // one float4 of the row at a time
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < FQ / 4; ++u) {
+            const float xv[4] = {B.x[u].x, B.x[u].y, B.x[u].z, B.x[u].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              // padded features (f >= d) hold 0 in X: adding -0 / +0 to the
+              // count slot leaves it unchanged (no per-feature branch)
+              const int f = min(FQ * q + 4 * u + e, d);
+              atomicAdd(so + f, -(double)xv[e]);
+              atomicAdd(sn + f, (double)xv[e]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        if (q == 0) {
+          atomicAdd(so + d, -1.0);
+          atomicAdd(sn + d, 1.0);
+        }
+      }
+    }
+    // queue: pair re-ranks from the front of the wave's segment, full scans
+    // from the back (k_fused16's layout, read by launch_resolve)
+    const bool enq = valid && kind != 0u && q == 0;
+    const uint64_t mq = __ballot(enq);
+    if (mq) {
+      const uint64_t m1 = __ballot(enq && kind == 1u);
+      const uint64_t m2 = mq & ~m1;
+      const uint64_t below = (1ull << lane) - 1ull;
+      if (enq) {
+        QEntry qe;
+        qe.row = (uint32_t)row;
+        qe.i1 = kind == 1u ? (uint32_t)lab1 : 0u;
+        qe.i2 = kind == 1u ? (uint32_t)lab2 : 0u;
+        qe.kind = kind;
+        const uint32_t pos = (kind == 1u) ? qn + (uint32_t)__popcll(m1 & below)
+                                          : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
+        wq[pos] = qe;
+      }
+      qn += (uint32_t)__popcll(m1);
+      qf += (uint32_t)__popcll(m2);
+    }
+  };
+
+  // this wave's tiles gw, gw + nw, ...: two register buffers, the next
+  // tile's loads in flight while one is processed (loads past the end read
+  // row n - 1 and are never used)
+  Buf b0, b1;
+  load(gw, b0);
+  // (tile + 2 nw stays below 2^32: ntiles < 2^28, nw < 2^16)
+  for (uint32_t tile = gw; tile < ntiles; tile += 2 * nw) {
+    load(tile + nw, b1);
+    process(tile, b0);
+    if (tile + nw >= ntiles) break;
+    load(tile + 2 * nw, b0);
+    process(tile + nw, b1);
+  }
+  if (lane == 0) {
+    A.qcount[2 * gw] = qn;
+    A.qcount[2 * gw + 1] = qf;
+  }
+}
+
+// Delta statistics (km_runtime.hip): mode 1 folds an iteration's all-reduced
+// deltas into the full sums and hands them to the update (full += stats;
+// stats = full); mode 0 keeps an iteration's full statistics (full = stats),
+// the base of the next deltas.  The SSE slot rides along (0 in delta mode).
+__global__ __launch_bounds__(256) void k_s1_apply(double* __restrict__ stats, double* __restrict__ full, int64_t len,
+                                                  int mode, const int* __restrict__ gate) {
+  if (*gate) return;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= len) return;
+  double v = stats[i];
+  if (mode == 1) v = full[i] + v;
+  full[i] = v;
+  stats[i] = v;
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_s1_apply(double* stats, double* full, int64_t len, int mode, const int* gate, hipStream_t s) {
+  if (len <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_s1_apply, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, stats, full, len, mode, gate);
+  return hipGetLastError();
+}
+
+// geometry only (never n): every rank of a job must take the same path, or
+// their delta and full statistics would be summed together
+bool s1_ok(const Geometry& g) {
+  if (g.dp % 32 || g.kp % 64) return false;
+  switch ((g.dp / 32) * 100 + g.kp / 32) {
+    case 202: case 204: case 206: case 208:
+    case 102: case 104: case 106: case 108: case 112: case 116:
+    case 402: case 404:
+      return true;
+    default:
+      return false;
+  }
+}
+
+static S1Geo s1_geo(const Geometry& g) {
+  S1Geo sg;
+  sg.nb = g.kp / 32;
+  sg.mb = ceil_log2_c(sg.nb);
+  sg.ns2 = g.dp / 32;
+  return sg;
+}
+
+size_t s1_table_entries(const Geometry& g) { return (size_t)32 << s1_geo(g).mb; }
+
+hipError_t launch_s1_color(const float* C32, const Geometry& g, int32_t* perm, const int* gate, hipStream_t s) {
+  const S1Geo sg = s1_geo(g);
+  if (g.k > 512) return hipErrorInvalidValue;
+  switch (g.dp) {
+    case 32: hipLaunchKernelGGL(k_s1_color<32>, dim3(1), dim3(512), 0, s, C32, g.k, g.dp, sg.nb, sg.mb, perm, gate); break;
+    case 64: hipLaunchKernelGGL(k_s1_color<64>, dim3(1), dim3(512), 0, s, C32, g.k, g.dp, sg.nb, sg.mb, perm, gate); break;
+    case 128: hipLaunchKernelGGL(k_s1_color<128>, dim3(1), dim3(512), 0, s, C32, g.k, g.dp, sg.nb, sg.mb, perm, gate); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_s1_prep(const double* C64, const float* C32, const Geometry& g, const int32_t* perm,
+                          const float* cmax, const float* xabs, const float* cabs, float* cft, float* cn2o,
+                          uint4* img, float* cst, const int* gate, hipStream_t s) {
+  const S1Geo sg = s1_geo(g);
+  const int nt = 32 << sg.mb;
+  hipLaunchKernelGGL(k_s1_prep, dim3(nt + 1), dim3(64), 0, s, C64, C32, g.k, g.d, g.dp, sg, perm, cmax, xabs, cabs,
+                     cft, cn2o, img, cst, gate);
+  return hipGetLastError();
+}
+
+hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, const uint4* img, const float* cn2o,
+                     const float* cft, const int32_t* perm, const float* cst, int32_t* labels,
+                     QEntry* queue, uint32_t* qcount, double* stats, int delta, int n_cu, QLayout* ql,
+                     const int* gate, hipStream_t s) {
+  ql->seg = 0;
+  ql->nwaves = 0;
+  if (g.n == 0) return hipSuccess;
+  const S1Geo sg = s1_geo(g);
+  const int nt = 32 << sg.mb;
+  const int64_t ntiles = (g.n + 15) / 16;
+  int64_t blocks = n_cu;
+  if (blocks > (ntiles + S1_WAVES - 1) / S1_WAVES) blocks = (ntiles + S1_WAVES - 1) / S1_WAVES;
+  const int nbk = (int)blocks;
+  const int64_t nw = (int64_t)nbk * S1_WAVES;
+  const uint32_t seg = (uint32_t)(((ntiles + nw - 1) / nw) * 16);
+  ql->seg = seg;
+  ql->nwaves = (uint32_t)nw;
+  S1Args a{X, xnorm, g.n, g.k, g.d, seg, img, cn2o, cft, perm, cst, labels, queue, qcount, stats, gate};
+  const size_t lds = (size_t)g.kp * g.dp * 2 + (size_t)nt * (g.dp + 4) * 4 + (size_t)g.kp * 4 + (size_t)nt * 4;
+#define KM_S1_CASE(NS2_, NB_)                                                                                   \
+  case NS2_ * 100 + NB_:                                                                                        \
+    if (delta)                                                                                                  \
+      KM_TIMED_LAUNCH((k_s1<NS2_, NB_, 1>), dim3(nbk), dim3(S1_WAVES * 64), lds, s, a);                         \
+    else                                                                                                        \
+      KM_TIMED_LAUNCH((k_s1<NS2_, NB_, 0>), dim3(nbk), dim3(S1_WAVES * 64), lds, s, a);                         \
+    break;
+  switch (sg.ns2 * 100 + sg.nb) {
+    KM_S1_CASE(2, 2) KM_S1_CASE(2, 4) KM_S1_CASE(2, 6) KM_S1_CASE(2, 8)
+    KM_S1_CASE(1, 2) KM_S1_CASE(1, 4) KM_S1_CASE(1, 6) KM_S1_CASE(1, 8) KM_S1_CASE(1, 12) KM_S1_CASE(1, 16)
+    KM_S1_CASE(4, 2) KM_S1_CASE(4, 4)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef KM_S1_CASE
+  return hipGetLastError();
+}
+
+}  // namespace km

@@ -219,26 +219,41 @@ class LabelsRDD(LocalRDD):
     """``predict``'s result: an RDD-like of Python ints in input order.
 
     The labels stay sharded (each rank holds its own rows' labels, its row
-    block of the input) until an action needs them all: ``collect()`` /
-    ``to_numpy()`` gather them (every rank runs the driver program, so every
-    rank gets the whole list, as Spark's driver does), ``count()`` sums the
-    shard lengths, ``local()`` is this rank's shard with no communication."""
+    block of the input) until an action needs them:
 
-    def __init__(self, local_labels: np.ndarray, comm: Communicator):
+    * ``collect()`` / ``to_numpy()`` bring them to the driver, as Spark's
+      collect() does: rank 0 gathers every rank's shard (one gather of N
+      int32, not an all-gather of N per rank), the other ranks get ``[]`` /
+      an empty array.  ``everywhere=True`` (per call, or for the object at
+      construction) gives every rank the whole list (one all-gather);
+    * ``count()`` sums the shard lengths;
+    * ``local()`` is this rank's shard with no communication."""
+
+    def __init__(self, local_labels: np.ndarray, comm: Communicator, everywhere: bool = False):
         self._local = local_labels
         self._comm = comm
-        self._all = None
+        self._everywhere = everywhere
+        self._all = None     # every rank's labels (everywhere)
+        self._root = None    # the driver's copy (rank 0)
         super().__init__([])
 
-    def _gather(self) -> np.ndarray:
-        if self._all is None:
-            self._all = np.concatenate(self._comm.allgather_array(self._local)) if self._comm.world > 1 \
-                else self._local
-            self._parts = [self._all.tolist()]
-        return self._all
+    def _gather(self, everywhere: Optional[bool]) -> np.ndarray:
+        ev = self._everywhere if everywhere is None else everywhere
+        if self._comm.world == 1:
+            return self._local
+        if ev:
+            if self._all is None:
+                self._all = np.concatenate(self._comm.allgather_array(self._local))
+            return self._all
+        if self._all is not None:
+            return self._all if self._comm.rank == 0 else self._local[:0]
+        if self._root is None:
+            parts = self._comm.gather_array(self._local, root=0)
+            self._root = np.concatenate(parts) if parts is not None else self._local[:0]
+        return self._root
 
-    def collect(self) -> list:
-        return self._gather().tolist()
+    def collect(self, everywhere: Optional[bool] = None) -> list:
+        return self._gather(everywhere).tolist()
 
     def count(self) -> int:
         if self._comm.world > 1:
@@ -252,8 +267,8 @@ class LabelsRDD(LocalRDD):
         """This rank's labels (rows [row0, row0 + n_local) of the input)."""
         return self._local
 
-    def to_numpy(self) -> np.ndarray:
-        return self._gather()
+    def to_numpy(self, everywhere: Optional[bool] = None) -> np.ndarray:
+        return self._gather(everywhere)
 
 
 def _ref_to(obj):
@@ -385,5 +400,6 @@ class KMeans:
         run.engine.set_centroids(np.asarray(self.centroids, dtype=np.float64))
         labels = LabelsRDD(run.engine.predict(), comm)
         if sc is not None and hasattr(sc, "_jsc") and hasattr(rdd, "getNumPartitions"):
-            return sc.parallelize(labels.collect(), rdd.getNumPartitions())  # a real SparkContext
+            # a real SparkContext (every rank's driver program parallelizes the whole list)
+            return sc.parallelize(labels.collect(everywhere=True), rdd.getNumPartitions())
         return labels

@@ -56,8 +56,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--screen", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
-                   help="fused-path screen (km_set_screen): -1 the runtime's per-batch choice "
+    p.add_argument("--screen", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4],
+                   help="fused-path screen (km_set_screen): -1 the runtime's choice (4 = k_s1 where the "
+                        "geometry has it), 0/1 fp16x3 k_fused16 with full statistics every iteration "
                         "(2, 3: diagnostic library only)")
     p.add_argument("--sse", type=int, default=None, choices=[0, 1],
                    help="compute_sse (kmeans_spark.py:38); default: on for c4, whose BASELINE config "
@@ -239,6 +240,21 @@ def main():
             roof = {"bound": "mfma", "achieved": ach, "peak": F16_DENSE_TFLOPS, "unit": "TFLOP/s",
                     "frac": ach / F16_DENSE_TFLOPS, "traffic": traffic, "kernel": kname,
                     "peak_note": f"dense f16 MFMA 2516.6 TF; achieved = {nx}*2*n*k*d per launch / avg launch time"}
+    elif info["path"] == 2 and dom == "assign" and screen == 4:
+        # k_s1 (km_screen1.hip): one fp16 MFMA per product (1.3 ms of MFMA at
+        # c3 against 3.2 ms of HBM at the spec peak), candidates re-scored in
+        # fp32, delta statistics: bound by HBM, the rows read once
+        t_mfma = flops_launch / (F16_DENSE_TFLOPS * 1e12)
+        b_alg = n_local * d * 4
+        t_hbm = b_alg / (HBM_PEAK_GBS * 1e9)
+        ach = b_alg / avg_s / 1e9
+        roof = {"bound": "hbm" if t_hbm >= t_mfma else "mfma", "achieved": ach, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                "kernel": "k_s1 (one fp16 MFMA per product, fp32 re-score of candidates, delta statistics)",
+                "bytes_note": "algorithmic N*d*4 per launch (X read once, SURVEY 8d); the kernel also reads the "
+                              "previous label and the row-norm bound (8 B per row); MFMA time at one fp16 MFMA "
+                              f"per product {t_mfma * 1e3:.2f} ms vs {t_hbm * 1e3:.2f} ms HBM at 8 TB/s",
+                "tflops": flops_launch / avg_s / 1e12, "tflops_frac_f16_dense": flops_launch / avg_s / 1e12 / F16_DENSE_TFLOPS}
     elif info["path"] == 2 and dom == "assign":
         ach = flops_launch / avg_s / 1e12
         # the fused screen runs on v_mfma_f32_16x16x32_f16 where dp is a
@@ -276,6 +292,8 @@ def main():
             "empty_repairs_on_device": run.device_repairs,
             "screen": screen,
             "arith": ("fp16 MFMA screen (balanced image, pairwise bound)" if screen in (2, 3) else
+                      "one fp16 MFMA per product, candidates re-scored in fp32 with a rigorous bound, float64 "
+                      "delta statistics" if screen == 4 else
                       "fp16x3 MFMA screen with a rigorous bound") +
                      ", float64 exact re-rank of ambiguous points, float64 partial sums",
         }

@@ -57,7 +57,9 @@ def _rank_main(rank, world, port, name, q):
         buf = io.StringIO()
         with contextlib.redirect_stdout(buf):
             km.fit(rdd, sc)
-        labels = np.array(km.predict(rdd, sc).collect())
+        pred = km.predict(rdd, sc)
+        # collect(): to the driver (rank 0) only; everywhere=True: every rank
+        labels = (np.array(pred.collect()), np.array(pred.collect(everywhere=True)))
         assert km._runner.engine.distributed
         assert km._runner.device_repair == 2
         q.put((rank, km.centroids, km.sse_history, labels, buf.getvalue(), km._runner.pl.n_local,
@@ -91,7 +93,8 @@ def test_two_ranks_on_gpu_match_reference(golden, name):
     for rank, C, sse, labels, out, _, reps in res:
         np.testing.assert_allclose(C, g["centroids"], rtol=1e-9, atol=1e-9)
         np.testing.assert_allclose(sse, g["sse_history"], rtol=1e-9)
-        np.testing.assert_array_equal(labels, g["labels"])
+        np.testing.assert_array_equal(labels[0], g["labels"] if rank == 0 else g["labels"][:0])
+        np.testing.assert_array_equal(labels[1], g["labels"])
         if name in ("empty", "c5_poor"):
             assert reps > 0, "the empty clusters were not repaired on the device"
     assert res[0][4] and not res[1][4]  # only rank 0 logs

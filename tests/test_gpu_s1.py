@@ -1,0 +1,277 @@
+"""The one-MFMA screen with in-kernel re-scoring and delta statistics
+(k_s1, km_set_screen mode 4 = KM_SCREEN_S1; csrc/km_screen1.hip).
+
+Reference: kmeans_spark.py:147-159 (np.argmin of np.linalg.norm(C - x,
+axis=1), first minimum) and :169-206 (per-cluster sums, mean update).
+
+Bars: labels bit-identical to the oracle's float64 argmin (its NumPy order
+and tie-break) -- the screen only proposes candidates, every label it
+decides carries a rigorous certificate, the rest go to the float64
+resolvers; centroids at 1e-9 relative against the oracle after several
+iterations, whose statistics after the first one are carried as deltas (the
+rows that changed clusters) on top of the first iteration's full sums.
+
+Predict runs k_s1 in labels-only mode (every geometry with an instance);
+fit runs it from the second iteration on (the first one, after new
+centroids, runs the fp16x3 screen with full statistics).  compute_sse keeps
+the full-statistics screen, so these fits run with it off.
+"""
+import numpy as np
+import pytest
+
+from oracle import kmeans_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+S1 = 4  # KM_SCREEN_S1 (include/kmeans_amd.h)
+SEED = 1234  # empty-cluster repair seed (the reference reads int(time.time()), kmeans_spark.py:196)
+
+
+def _km():
+    import kmeans_amd
+    return kmeans_amd
+
+
+def _engine(mode=-1):
+    from kmeans_amd.comm import Communicator
+    from kmeans_amd.engine import make_engine
+    eng = make_engine(Communicator())
+    eng.set_screen(mode)
+    return eng
+
+
+def _predict(X, C, mode=-1):
+    eng = _engine(mode)
+    eng.load_host(X.astype(np.float32))
+    eng.set_centroids(C)
+    return eng.predict(), eng
+
+
+def _fit(X, C0, iters, mode=-1, compute_sse=False):
+    ka = _km()
+    from kmeans_amd.engine import make_engine
+
+    def factory(comm):
+        eng = make_engine(comm)
+        eng.set_screen(mode)
+        return eng
+
+    class Forced(ka.KMeans):
+        _engine_factory = staticmethod(factory)
+
+        def _initialize_centroids(self, run):
+            return C0.copy()
+
+        def _empty_seed(self):
+            return SEED
+
+    km = Forced(k=len(C0), max_iter=iters, tolerance=1e-12, compute_sse=compute_sse)
+    km.verbose = False
+    km.fit(X)
+    return km
+
+
+def _blobs(n, d, centers, seed, box=10.0, std=1.0):
+    rng = np.random.default_rng(seed)
+    C = rng.uniform(-box, box, (centers, d))
+    lab = rng.integers(0, centers, n)
+    return (C[lab] + std * rng.standard_normal((n, d))).astype(np.float32).astype(np.float64)
+
+
+def _check_fit(X, C0, iters):
+    km = _fit(X, C0, iters)
+    eng = km._runner.engine
+    assert eng.screen() == S1, "k_s1 not selected for this geometry"
+    ref = orc.lloyd_fit(X, len(C0), iters, 1e-12, 0, False, 1, init_centroids=C0, empty_seed=lambda: SEED)
+    np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
+    # labels of the last pass (the centroids it read: those after iters - 1)
+    C_prev = orc.lloyd_fit(X, len(C0), iters - 1, 1e-12, 0, False, 1, init_centroids=C0, empty_seed=lambda: SEED)["centroids"]
+    np.testing.assert_array_equal(eng.labels(), orc.assign(X, C_prev)[0])
+    # the sums behind the last update: counts equal the label histogram
+    np.testing.assert_array_equal(km._runner.last["counts"], np.bincount(eng.labels(), minlength=len(C0)))
+    return km
+
+
+# -- predict (labels only) on the screen's hard cases --------------------------------
+
+def test_c3_class_selects_s1():
+    X = _blobs(4000, 64, 64, seed=1)
+    C0 = X[:256].copy()
+    km = _fit(X, C0, 2)
+    assert km._runner.engine.screen() == S1
+
+
+@pytest.mark.parametrize("n,d,k,centers", [
+    (60000, 64, 256, 256),   # c3 shape: dp 64, kp 256
+    (30000, 20, 100, 50),    # dp 32, kp 128 (pads)
+    (30000, 32, 512, 300),   # dp 32, kp 512 (16 members per chain)
+    (20000, 128, 128, 128),  # dp 128, kp 128
+    (20000, 64, 70, 40),     # kp 128, 58 pad slots
+])
+def test_predict_blobs_vs_oracle(n, d, k, centers):
+    X = _blobs(n, d, centers, seed=3 + d)
+    C = X[np.random.default_rng(1).choice(n, k, replace=False)]
+    labels, _ = _predict(X, C)
+    np.testing.assert_array_equal(labels, orc.assign(X, C)[0])
+
+
+def test_predict_points_on_and_near_bisectors():
+    # close centroid pairs (separation 0.05 .. 5) and points at signed
+    # distances 1e-7 .. 1 from their bisector planes: exact ties, one-ulp
+    # gaps and everything the fp32 re-score must hand to float64
+    rng = np.random.default_rng(17)
+    d, k = 64, 256
+    C = rng.uniform(-10, 10, (k, d))
+    pairs = rng.permutation(k)[:128].reshape(64, 2)
+    for a, b in pairs:
+        u = rng.standard_normal(d)
+        C[b] = C[a] + u / np.linalg.norm(u) * 10 ** rng.uniform(-1.3, 0.7)
+    C = C.astype(np.float32).astype(np.float64)
+    rows = []
+    for a, b in pairs:
+        m = 0.5 * (C[a] + C[b])
+        e = (C[b] - C[a]) / np.linalg.norm(C[b] - C[a])
+        t = np.concatenate([[0.0], 10 ** rng.uniform(-7, 0, 150)]) * rng.choice([-1, 1], 151)
+        tang = rng.standard_normal((151, d)) * rng.uniform(0, 3, (151, 1))
+        tang -= np.outer(tang @ e, e)
+        rows.append(m + tang + np.outer(t, e))
+    X = np.concatenate(rows).astype(np.float32).astype(np.float64)
+    labels, _ = _predict(X, C)
+    np.testing.assert_array_equal(labels, orc.assign(X, C)[0])
+
+
+@pytest.mark.parametrize("nb", [128, 127])
+def test_predict_one_ulp_duplicates(nb):
+    X = _blobs(20000, 64, 64, seed=75)
+    base = X[np.random.default_rng(69).choice(len(X), nb, replace=False)]
+    C = np.concatenate([base, np.nextafter(base, np.inf)])
+    labels, _ = _predict(X, C)
+    np.testing.assert_array_equal(labels, orc.assign(X, C)[0])
+
+
+def test_predict_duplicate_centroids_lowest_index():
+    X = _blobs(8000, 64, 40, seed=9)
+    C = X[np.random.default_rng(0).choice(len(X), 256, replace=False)]
+    C[10] = C[3]
+    C[200] = C[3]
+    labels, _ = _predict(X, C)
+    np.testing.assert_array_equal(labels, orc.assign(X, C)[0])
+    assert not np.any(labels == 10) and not np.any(labels == 200)
+
+
+def test_predict_far_from_origin():
+    # |c_f| ~ 1000, unit spread: the one-MFMA bound (~ 2^-9 ||c|| ||x||) is
+    # far wider than the gaps, most rows have more candidates than the
+    # kernel re-scores and go to the float64 scan; labels stay exact
+    X = _blobs(20000, 64, 128, seed=5, box=1000.0, std=1.0)
+    C = X[np.random.default_rng(2).choice(len(X), 256, replace=False)]
+    labels, _ = _predict(X, C)
+    np.testing.assert_array_equal(labels, orc.assign(X, C)[0])
+
+
+def test_predict_features_across_magnitudes():
+    rng = np.random.default_rng(8)
+    scale = 10.0 ** np.linspace(-9, 3, 64)
+    X = (_blobs(20000, 64, 64, seed=9) * scale).astype(np.float32).astype(np.float64)
+    C = X[rng.choice(len(X), 200, replace=False)]
+    labels, _ = _predict(X, C)
+    np.testing.assert_array_equal(labels, orc.assign(X, C)[0])
+
+
+def test_predict_zero_rows_and_zero_centroids():
+    # keys of exactly 0 (x = 0, c = 0): packed keys are tiny or signed zeros
+    X = _blobs(6000, 64, 32, seed=4)
+    X[::7] = 0.0
+    C = X[np.random.default_rng(5).choice(len(X), 256, replace=False)]
+    C[0] = 0.0
+    C[77] = 0.0
+    labels, _ = _predict(X, C)
+    np.testing.assert_array_equal(labels, orc.assign(X, C)[0])
+
+
+def test_predict_matches_full_screen_on_many_seeds():
+    # the same geometry through k_s1 (auto) and k_fused16 (forced mode 1)
+    for seed in range(4):
+        X = _blobs(20000, 64, 200, seed=100 + seed)
+        C = X[np.random.default_rng(seed).choice(len(X), 256, replace=False)] + 0.3
+        a, _ = _predict(X, C, -1)
+        b, _ = _predict(X, C, 1)
+        np.testing.assert_array_equal(a, b)
+
+
+# -- fits: delta statistics across iterations ------------------------------------------
+
+def test_fit_c3_shape_delta_iterations():
+    X = _blobs(60000, 64, 256, seed=11)
+    C0 = X[np.random.default_rng(12).choice(len(X), 256, replace=False)]
+    km = _check_fit(X, C0, 8)
+    # the certificate settles nearly every row in the kernel (c3 data: about
+    # 88% by the screen alone, the rest by the fp32 re-score)
+    last = km._runner.last
+    assert last["q_full"] + last["q_rerank"] < 0.002 * len(X), last
+
+
+def test_fit_noise_delta_iterations():
+    # randn: no cluster structure, many rows change clusters every iteration
+    rng = np.random.RandomState(42)
+    X = rng.randn(30000, 64).astype(np.float32).astype(np.float64)
+    C0 = X[np.random.default_rng(2).choice(len(X), 256, replace=False)]
+    _check_fit(X, C0, 6)
+
+
+@pytest.mark.parametrize("n,d,k,centers", [
+    (30000, 20, 100, 50),
+    (30000, 32, 512, 300),
+    (20000, 128, 128, 128),
+    (20000, 64, 70, 40),
+])
+def test_fit_shapes_delta_iterations(n, d, k, centers):
+    X = _blobs(n, d, centers, seed=21 + k)
+    C0 = X[np.random.default_rng(22).choice(n, k, replace=False)]
+    _check_fit(X, C0, 5)
+
+
+def test_fit_far_from_origin_delta_iterations():
+    X = _blobs(20000, 64, 128, seed=5, box=1000.0, std=1.0)
+    C0 = X[np.random.default_rng(2).choice(len(X), 256, replace=False)]
+    _check_fit(X, C0, 3)
+
+
+def test_delta_fit_equals_full_statistics_fit():
+    # every iteration with full statistics (mode 1: k_fused16) against the
+    # default (k_s1 with deltas from the second iteration): identical labels
+    # and counts, centroids equal up to float64 summation order
+    X = _blobs(40000, 64, 256, seed=31)
+    C0 = X[np.random.default_rng(32).choice(len(X), 256, replace=False)]
+    a = _fit(X, C0, 6, mode=-1)
+    b = _fit(X, C0, 6, mode=1)
+    assert a._runner.engine.screen() == S1 and b._runner.engine.screen() == 1
+    np.testing.assert_array_equal(a._runner.engine.labels(), b._runner.engine.labels())
+    np.testing.assert_array_equal(a._runner.last["counts"], b._runner.last["counts"])
+    np.testing.assert_allclose(a.centroids, b.centroids, rtol=1e-12, atol=1e-12)
+
+
+def test_fit_then_predict_then_fit_again():
+    # predict overwrites the labels the deltas refer to: the next fit must
+    # start from full statistics again (delta_ready reset), and stay exact
+    X = _blobs(20000, 64, 256, seed=41)
+    C0 = X[np.random.default_rng(42).choice(len(X), 256, replace=False)]
+    km = _fit(X, C0, 3)
+    run = km._runner
+    km.predict(X)
+    km.max_iter = 3
+    run.engine.set_centroids(np.asarray(km.centroids, dtype=np.float64))
+    run.run(km, None, 3)
+    C3 = orc.lloyd_fit(X, 256, 3, 1e-12, 0, False, 1, init_centroids=C0, empty_seed=lambda: SEED)["centroids"]
+    ref = orc.lloyd_fit(X, 256, 3, 1e-12, 0, False, 1, init_centroids=C3, empty_seed=lambda: SEED)
+    np.testing.assert_allclose(run.engine.get_centroids(0), ref["centroids"], rtol=1e-9, atol=1e-9)
+
+
+def test_compute_sse_keeps_full_statistics():
+    X = _blobs(20000, 64, 256, seed=51)
+    C0 = X[np.random.default_rng(52).choice(len(X), 256, replace=False)]
+    km = _fit(X, C0, 3, compute_sse=True)
+    assert km._runner.engine.screen() != S1
+    ref = orc.lloyd_fit(X, 256, 3, 1e-12, 0, True, 1, init_centroids=C0, empty_seed=lambda: SEED)
+    np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)

@@ -34,7 +34,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert declared == set(_lib.exported_symbols()), declared ^ set(_lib.exported_symbols())
-    assert lib.km_abi_version() == 4
+    assert lib.km_abi_version() == 5
 
 
 def test_product_library_has_no_diagnostic_kernels():
@@ -462,7 +462,10 @@ def _rank_main(rank, world, port, name, q, device_repair=False):
         g = load_golden(name)
         km, out, labels = _fit(g, inject=(name in INJECTED))
         run = km._runner
-        q.put((rank, km.centroids, km.sse_history, labels, out, (run.device_repair, run.device_repairs)))
+        pred = km.predict(g["X"])
+        views = {"root": np.asarray(labels), "everywhere": np.asarray(pred.collect(everywhere=True)),
+                 "local": pred.local().copy(), "row0": run.pl.row0, "count": pred.count()}
+        q.put((rank, km.centroids, km.sse_history, views, out, (run.device_repair, run.device_repairs)))
     finally:
         dist.destroy_process_group()
 
@@ -486,10 +489,16 @@ def _run_ranks(world, name, device_repair=False):
 def test_two_ranks_gloo_match_single_rank(golden, name):
     g = golden(name)
     res = _run_ranks(2, name)
-    for rank, C, sse, labels, out, _ in res:
+    for rank, C, sse, v, out, _ in res:
         np.testing.assert_allclose(C, g["centroids"], rtol=1e-9, atol=1e-9)
         np.testing.assert_allclose(sse, g["sse_history"], rtol=1e-9)
-        np.testing.assert_array_equal(labels, g["labels"])
+        # collect(): the driver (rank 0) gets every label, the others none;
+        # everywhere=True: every rank; local(): the rank's own row block
+        np.testing.assert_array_equal(v["root"], g["labels"] if rank == 0 else g["labels"][:0])
+        np.testing.assert_array_equal(v["everywhere"], g["labels"])
+        np.testing.assert_array_equal(v["local"], g["labels"][v["row0"]:v["row0"] + len(v["local"])])
+        assert v["count"] == len(g["labels"])
+    assert sum(len(r[3]["local"]) for r in res) == len(g["labels"])
     assert res[0][4] and not res[1][4]  # only rank 0 logs, like the single driver
 
 
@@ -503,11 +512,12 @@ def test_device_repair_protocol_over_gloo_ranks(golden, world, name):
     from test_gpu_parity import assert_logs_match
     g = golden(name)
     res = _run_ranks(world, name, device_repair=True)
-    for rank, C, sse, labels, out, (mode, repairs) in res:
+    for rank, C, sse, v, out, (mode, repairs) in res:
         assert mode == (2 if world > 1 else 1) and repairs >= 1, (mode, repairs)
         np.testing.assert_allclose(C, g["centroids"], rtol=1e-9, atol=1e-9)
         np.testing.assert_allclose(sse, g["sse_history"], rtol=1e-9)
-        np.testing.assert_array_equal(labels, g["labels"])
+        np.testing.assert_array_equal(v["everywhere"], g["labels"])
+        np.testing.assert_array_equal(v["root"], g["labels"] if rank == 0 else g["labels"][:0])
     assert_logs_match(res[0][4], g["stdout"])
     assert all(not r[4] for r in res[1:])
 
