@@ -569,6 +569,10 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
                           T.stop_tol, T.dev_repair, 1, T.C32n, T.cmaxn, DP, T.kp);
     if (threadIdx.x == 0)
       T.st->q_rerank = (int32_t)__hip_atomic_load(T.done + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (T.qout && threadIdx.x == 0) {
+    // the separate update launch reports the queued rows from qcount (one segment)
+    T.qout[0] = __hip_atomic_load(T.done + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    T.qout[1] = 0u;
   }
   if (threadIdx.x == 0) {
     T.done[0] = 0u;

@@ -101,6 +101,8 @@ struct km_ctx {
   uint4* s1_img = nullptr;       // fragment-linear fp16 image of -2 s c
   float* s1_cst = nullptr;       // bound constants
   double* stats_full = nullptr;  // the full sums the deltas apply to
+  uint2* chg = nullptr;          // k_s1 change list (capacity n), {row, old << 16 | new}
+  uint32_t* chg_ctr = nullptr;   // its length (zeroed by km::launch_s1_apply)
   bool delta_ready = false;      // labels and stats_full describe one assignment
   int stats_pending = 0;         // the last assign left 0 nothing, 1 full sums, 2 deltas in stats
   float* bal = nullptr;  // fast screen: image error maxima (2 floats)
@@ -280,6 +282,8 @@ void free_centroids(km_ctx* c) {
   dfree(c->s1_img);
   dfree(c->s1_cst);
   dfree(c->stats_full);
+  dfree(c->chg);
+  dfree(c->chg_ctr);
   c->s1 = false;
   c->delta_ready = false;
   c->stats_pending = 0;
@@ -414,6 +418,7 @@ km::SmallTail small_tail(km_ctx* c) {
   t.qctr = c->small_ctr;
   t.done = c->small_ctr + 1;
   t.kp = c->g.kp;
+  t.qout = c->qcount;
   return t;
 }
 
@@ -444,8 +449,8 @@ int apply_stats(km_ctx* c) {
   if (!c->s1) return KM_OK;
   const bool keep = kind == 2 || (kind == 1 && !c->want_sse);
   if (keep)
-    KM_HIP(km::launch_s1_apply(c->stats, c->stats_full, (int64_t)stats_len(c->g), kind == 2 ? 1 : 0, c->gate,
-                               c->stream));
+    KM_HIP(km::launch_s1_apply(c->stats, c->stats_full, (int64_t)stats_len(c->g), kind == 2 ? 1 : 0, c->chg_ctr,
+                               c->gate, c->stream));
   c->delta_ready = keep;
   return KM_OK;
 }
@@ -473,6 +478,7 @@ int run_assign(km_ctx* c, bool with_stats) {
     ProfScope ps(c, KM_K_ASSIGN, true);
     KM_HIP(km::launch_assign_small(c->X, g, c->C32, c->C64_cur, c->cmax, c->labels, c->stats, with_stats ? 1 : 0,
                                    sse ? 1 : 0, c->n_cu, c->gate, c->stream, small_tail(c)));
+    c->ql = km::QLayout{0, g.n > 0 ? 1u : 0u};  // its last workgroup leaves the queued rows in qcount[0]
     return KM_OK;
   }
   c->stats_pending = with_stats ? 1 : 0;
@@ -480,8 +486,8 @@ int run_assign(km_ctx* c, bool with_stats) {
     {
       ProfScope ps(c, KM_K_ASSIGN, true);
       KM_HIP(km::launch_s1(c->X, c->xnorm, g, c->s1_img, c->s1_cn2o, c->s1_cft, c->s1_perm, c->s1_cst,
-                           c->labels, c->queue, c->qcount, with_stats ? c->stats : nullptr, with_stats ? 1 : 0,
-                           c->n_cu, &c->ql, c->gate, c->stream));
+                           c->labels, c->queue, c->qcount, c->chg, c->chg_ctr, with_stats ? 1 : 0, c->n_cu,
+                           &c->ql, c->gate, c->stream));
     }
     {
       // the queued rows: near-ties of the re-scored candidates and the rows
@@ -491,6 +497,11 @@ int run_assign(km_ctx* c, bool with_stats) {
       KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels,
                                 with_stats ? c->stats : nullptr, c->n_cu, c->gate, c->stream, nullptr, nullptr, 0,
                                 with_stats ? 1 : 0));
+    }
+    if (with_stats) {
+      // the rows k_s1 moved between clusters (its change list) into the deltas
+      ProfScope ps(c, KM_K_STATS);
+      KM_HIP(km::launch_s1_delta(c->X, g, c->chg, c->chg_ctr, c->stats, c->n_cu, c->gate, c->stream));
     }
     c->stats_pending = with_stats ? 2 : 0;
     return KM_OK;
@@ -862,6 +873,9 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
       KM_HIP(hipMalloc(&c->s1_img, sizeof(_Float16) * kp * dp));
       KM_HIP(hipMalloc(&c->s1_cst, sizeof(float) * 8));
       KM_HIP(hipMalloc(&c->stats_full, sizeof(double) * stats_len(c->g)));
+      KM_HIP(hipMalloc(&c->chg, sizeof(uint2) * (size_t)std::max<int64_t>(c->g.n, 1)));
+      KM_HIP(hipMalloc(&c->chg_ctr, sizeof(uint32_t)));
+      KM_HIP(hipMemsetAsync(c->chg_ctr, 0, sizeof(uint32_t), c->stream));
     }
   }
   c->s1_recolor = true;

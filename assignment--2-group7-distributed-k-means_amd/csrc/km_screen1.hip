@@ -20,9 +20,10 @@
 //     double-buffered in registers: one wave's VALU work hides under the
 //     other's MFMAs and loads;
 //   * statistics: either none (predict) or DELTAS -- a row whose label did not
-//     change since the last iteration adds nothing; a changed row moves its
-//     x from the old cluster's float64 sums to the new one's (global float64
-//     atomics).  The runtime keeps the full sums (km_runtime.hip, "delta
+//     change since the last iteration adds nothing; a changed row is appended
+//     to a change list (row, old, new), and k_s1_delta moves its x from the
+//     old cluster's float64 sums to the new one's through an LDS table per
+//     workgroup.  The runtime keeps the full sums (km_runtime.hip, "delta
 //     statistics"), so the sums the update reads are the reference's
 //     reduceByKey sums over every row, exactly as a fresh pass would produce
 //     them up to float64 summation order.
@@ -262,7 +263,8 @@ struct S1Args {
   int32_t* labels;
   QEntry* queue;
   uint32_t* qcount;
-  double* stats;  // DELTA: [k][d+1] float64 deltas (sums, counts)
+  uint2* chg;          // DELTA: changed rows {row, old << 16 | new}
+  uint32_t* chg_ctr;   // DELTA: entries in chg (zeroed by k_s1_apply)
   const int* gate;
 };
 
@@ -312,7 +314,6 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
   const uint32_t nw = gridDim.x * S1_WAVES;
   QEntry* wq = A.queue + (size_t)gw * A.seg;
   uint32_t qn = 0, qf = 0;
-  const int d = A.d;
   // chain id bits of this lane's 8 accumulator positions (cb, i): chain 16 cb + 4 q + i
   const uint32_t qbits = (uint32_t)(4 * q) << MB;
 
@@ -420,13 +421,30 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) hk[cb][i] = mono(f2u(h[cb][i]) | qbits | ((uint32_t)(16 * cb + i) << MB));
 
-    // smallest head of the row and the candidate threshold T
-    int32_t ml = hk[0][0];
+    // the row's two smallest heads (m and the second candidate), then the
+    // candidate threshold T: the lane's lowest two (med3 keeps the middle of
+    // a sorted pair and a new value), merged over the quad
+    int32_t la = INT32_MAX, lb = INT32_MAX;
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ml = min(ml, hk[cb][i]);
-    const int32_t mki = quad_min_i(ml);
+      for (int i = 0; i < 4; ++i) {
+        lb = max(la, min(lb, hk[cb][i]));  // med3 (la <= lb)
+        la = min(la, hk[cb][i]);
+      }
+    {
+      auto p = __builtin_amdgcn_permlane16_swap((uint32_t)la, (uint32_t)la, false, false);
+      auto p2 = __builtin_amdgcn_permlane16_swap((uint32_t)lb, (uint32_t)lb, false, false);
+      int32_t a0 = (int32_t)p[0], a1 = (int32_t)p[1], b0 = (int32_t)p2[0], b1 = (int32_t)p2[1];
+      la = min(a0, a1);
+      lb = min(max(a0, a1), min(b0, b1));
+      p = __builtin_amdgcn_permlane32_swap((uint32_t)la, (uint32_t)la, false, false);
+      p2 = __builtin_amdgcn_permlane32_swap((uint32_t)lb, (uint32_t)lb, false, false);
+      a0 = (int32_t)p[0], a1 = (int32_t)p[1], b0 = (int32_t)p2[0], b1 = (int32_t)p2[1];
+      la = min(a0, a1);
+      lb = min(max(a0, a1), min(b0, b1));
+    }
+    const int32_t mki = la;
     const float m = u2f(unmono(mki));
     const float xn = B.xn;
     const float E = fmaf(e1, xn, e0);
@@ -456,22 +474,10 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     float U1 = FLT_MAX, L1 = FLT_MAX, Lo = FLT_MAX;
     const bool need = valid && !bad && !ovf && cnt >= 2u && cnt <= (uint32_t)S1_LMAX;
     if (__ballot(need) != 0ull) {
-      // candidates in ascending key order: round r takes the smallest head
-      // above the previous one; every lane of the wave re-scores (a row with
-      // no candidate left scores slot 0 and ignores it)
-      int32_t prev = INT32_MIN;
-#pragma unroll 1
-      for (int r = 0; r < S1_LMAX; ++r) {
-        const bool act = need && (uint32_t)r < cnt;
-        if (__ballot(act) == 0ull) break;
-        int32_t nl = INT32_MAX;
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) nl = min(nl, hk[cb][i] > prev ? hk[cb][i] : INT32_MAX);
-        const int32_t cur = quad_min_i(nl);
-        prev = cur;
-        const uint32_t sl = act ? (unmono(cur) & SLOTM) : 0u;
+      // fp32 re-score of candidate slot sl: bounds of ||x - c|| (unscaled).
+      // |Dt - D'| <= (FQ + 4) u D' <= 36 u D' (D' = ||x - c'||^2, FQ <= 32),
+      // then ||x - c|| = sqrt(D') +- g; sqrt and products: 8 u
+      auto partial = [&](uint32_t sl) {
         const float4* cp = reinterpret_cast<const float4*>(sCf + sl * CS + FQ * q);
         float acc = 0.0f;
 #pragma unroll
@@ -484,13 +490,14 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
           acc = fmaf(d2, d2, acc);
           acc = fmaf(d3, d3, acc);
         }
-        const float Dt = quad_sum(acc);
-        // |Dt - D'| <= (FQ + 4) u D' <= 36 u D' (D' = ||x - c'||^2, FQ <= 32),
-        // then ||x - c|| = sqrt(D') +- g; sqrt and products: 8 u
+        return acc;
+      };
+      // winner / others bookkeeping, select form throughout (DESIGN.md
+      // section 2: branchy running minima are miscompiled in divergent code
+      // on this toolchain)
+      auto take = [&](bool act, float Dt, uint32_t sl) {
         const float U = (sqrtf(Dt * (1.0f + 48.0f * U24)) + gam) * (1.0f + 8.0f * U24);
         const float L = (sqrtf(Dt * (1.0f - 48.0f * U24)) - gam) * (1.0f - 8.0f * U24);
-        // select form throughout (branchy running minima
-        // are miscompiled in divergent code on this toolchain)
         const bool w = act && U < U1;              // new winner
         const float Lc = w ? L1 : L;               // the displaced winner, or this one, joins the others
         const uint32_t sc = w ? s1 : sl;
@@ -500,6 +507,32 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
         U1 = w ? U : U1;
         L1 = w ? L : L1;
         s1 = w ? sl : s1;
+      };
+      // the first two candidates (every needy row has them) in one round:
+      // both tables' reads in flight together; rows without a need score
+      // slot 0 and ignore it
+      {
+        const uint32_t sa = need ? (unmono(mki) & SLOTM) : 0u;
+        const uint32_t sb = need ? (unmono(lb) & SLOTM) : 0u;
+        const float pa = partial(sa), pb = partial(sb);
+        take(need, quad_sum(pa), sa);
+        take(need, quad_sum(pb), sb);
+      }
+      // the rest in ascending key order: the smallest head above the last
+      int32_t prev = lb;
+#pragma unroll 1
+      for (int r = 2; r < S1_LMAX; ++r) {
+        const bool act = need && (uint32_t)r < cnt;
+        if (__ballot(act) == 0ull) break;
+        int32_t nl = INT32_MAX;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) nl = min(nl, hk[cb][i] > prev ? hk[cb][i] : INT32_MAX);
+        const int32_t cur = quad_min_i(nl);
+        prev = cur;
+        const uint32_t sl = act ? (unmono(cur) & SLOTM) : 0u;
+        take(act, quad_sum(partial(sl)), sl);
       }
     }
     // decision: 0 decided, 1 pair re-rank (k_rerank2), 2 full scan (k_fullscan)
@@ -519,43 +552,16 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
       // (a previous label is always a cluster index; clamped so that a
       // corrupt one can never address outside the sums)
       const int32_t old = (int32_t)min((uint32_t)B.old, (uint32_t)(A.k - 1));
-      const bool changed = decided && lab1 != old;
-      if (__ballot(changed) != 0ull && changed) {
-        if (q == 0) A.labels[row] = lab1;
-        double* so = A.stats + (size_t)old * (d + 1);
-        double* sn = A.stats + (size_t)lab1 * (d + 1);
-        if (d == DP) {
-          // no padding: one base per lane, the features at constant offsets
-          double* po = so + FQ * q;
-          double* pn = sn + FQ * q;
-#pragma unroll
-          for (int u = 0; u < FQ / 4; ++u) {
-            const float xv[4] = {B.x[u].x, B.x[u].y, B.x[u].z, B.x[u].w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              atomicAdd(po + 4 * u + e, -(double)xv[e]);
-              atomicAdd(pn + 4 * u + e, (double)xv[e]);
-            }
-            __builtin_amdgcn_sched_barrier(0);  // one float4 of the row at a time
-          }
-        } else {
-#pragma unroll
-          for (int u = 0; u < FQ / 4; ++u) {
-            const float xv[4] = {B.x[u].x, B.x[u].y, B.x[u].z, B.x[u].w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              // padded features (f >= d) hold 0 in X: adding -0 / +0 to the
-              // count slot leaves it unchanged (no per-feature branch)
-              const int f = min(FQ * q + 4 * u + e, d);
-              atomicAdd(so + f, -(double)xv[e]);
-              atomicAdd(sn + f, (double)xv[e]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-        if (q == 0) {
-          atomicAdd(so + d, -1.0);
-          atomicAdd(sn + d, 1.0);
+      const bool changed = decided && lab1 != old && q == 0;  // one lane per row
+      const uint64_t mc = __ballot(changed);
+      if (mc) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(A.chg_ctr, (uint32_t)__popcll(mc));
+        base = __shfl(base, 0);
+        if (changed) {
+          A.labels[row] = lab1;
+          A.chg[base + (uint32_t)__popcll(mc & ((1ull << lane) - 1ull))] =
+              make_uint2(row, ((uint32_t)old << 16) | (uint32_t)lab1);
         }
       }
     }
@@ -606,9 +612,11 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
 // stats = full); mode 0 keeps an iteration's full statistics (full = stats),
 // the base of the next deltas.  The SSE slot rides along (0 in delta mode).
 __global__ __launch_bounds__(256) void k_s1_apply(double* __restrict__ stats, double* __restrict__ full, int64_t len,
-                                                  int mode, const int* __restrict__ gate) {
+                                                  int mode, uint32_t* __restrict__ chg_ctr,
+                                                  const int* __restrict__ gate) {
   if (*gate) return;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0 && chg_ctr) *chg_ctr = 0u;  // the change list is consumed (k_s1_delta ran before)
   if (i >= len) return;
   double v = stats[i];
   if (mode == 1) v = full[i] + v;
@@ -616,12 +624,78 @@ __global__ __launch_bounds__(256) void k_s1_apply(double* __restrict__ stats, do
   stats[i] = v;
 }
 
+// The change list of k_s1 into the delta statistics: each workgroup takes a
+// contiguous slice (at least S1D_MIN entries, so a short list wakes few
+// workgroups and flushes few tables), moves each changed row's x from its
+// old cluster to its new one in an LDS float64 table [k][d+1] (lanes over
+// features: consecutive banks), 8 rows per wave in flight, then adds the
+// table's non-zero entries to the statistics with global atomics.
+constexpr uint32_t S1D_MIN = 2048;
+constexpr int S1D_ROWS = 8;
+__global__ __launch_bounds__(1024) void k_s1_delta(const float* __restrict__ X, int dp, int d, int k,
+                                                   const uint2* __restrict__ chg,
+                                                   const uint32_t* __restrict__ chg_ctr, double* __restrict__ stats,
+                                                   const int* __restrict__ gate) {
+  if (*gate) return;
+  const uint32_t nc = *chg_ctr;
+  const uint32_t per = max(S1D_MIN, (nc + gridDim.x - 1u) / gridDim.x);
+  const uint32_t e0 = blockIdx.x * per;
+  if (e0 >= nc) return;
+  const uint32_t e1 = min(nc, e0 + per);
+  extern __shared__ double tab[];  // [k][d + 1]
+  const int d1 = d + 1;
+  for (int i = threadIdx.x; i < k * d1; i += blockDim.x) tab[i] = 0.0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  for (uint32_t e = e0 + (uint32_t)wave * S1D_ROWS; e < e1; e += (uint32_t)nwv * S1D_ROWS) {
+    uint2 c[S1D_ROWS];
+#pragma unroll
+    for (int r = 0; r < S1D_ROWS; ++r) c[r] = chg[min(e + (uint32_t)r, e1 - 1u)];
+    for (int f0 = 0; f0 < d; f0 += 64) {
+      const int f = f0 + lane;
+      float x[S1D_ROWS];
+#pragma unroll
+      for (int r = 0; r < S1D_ROWS; ++r) x[r] = f < d ? X[(size_t)c[r].x * dp + f] : 0.0f;
+#pragma unroll
+      for (int r = 0; r < S1D_ROWS; ++r) {
+        if (e + (uint32_t)r >= e1 || f >= d) continue;
+        const uint32_t old = c[r].y >> 16, nw = c[r].y & 0xFFFFu;
+        atomicAdd(tab + (size_t)old * d1 + f, -(double)x[r]);
+        atomicAdd(tab + (size_t)nw * d1 + f, (double)x[r]);
+      }
+    }
+    if (lane == 0)
+#pragma unroll
+      for (int r = 0; r < S1D_ROWS; ++r) {
+        if (e + (uint32_t)r >= e1) continue;
+        atomicAdd(tab + (size_t)(c[r].y >> 16) * d1 + d, -1.0);
+        atomicAdd(tab + (size_t)(c[r].y & 0xFFFFu) * d1 + d, 1.0);
+      }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < k * d1; i += blockDim.x) {
+    const double v = tab[i];
+    if (v != 0.0) atomicAdd(stats + i, v);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-hipError_t launch_s1_apply(double* stats, double* full, int64_t len, int mode, const int* gate, hipStream_t s) {
+hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_ctr,
+                           double* stats, int n_cu, const int* gate, hipStream_t s) {
+  if (g.n == 0) return hipSuccess;
+  const size_t lds = (size_t)g.k * (g.d + 1) * 8;
+  if (lds > 160 * 1024 || g.k > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_s1_delta, dim3(n_cu), dim3(1024), lds, s, X, g.dp, g.d, g.k, chg, chg_ctr, stats, gate);
+  return hipGetLastError();
+}
+
+hipError_t launch_s1_apply(double* stats, double* full, int64_t len, int mode, uint32_t* chg_ctr, const int* gate,
+                           hipStream_t s) {
   if (len <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_s1_apply, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, stats, full, len, mode, gate);
+  hipLaunchKernelGGL(k_s1_apply, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, stats, full, len, mode, chg_ctr,
+                     gate);
   return hipGetLastError();
 }
 
@@ -673,8 +747,8 @@ hipError_t launch_s1_prep(const double* C64, const float* C32, const Geometry& g
 
 hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, const uint4* img, const float* cn2o,
                      const float* cft, const int32_t* perm, const float* cst, int32_t* labels,
-                     QEntry* queue, uint32_t* qcount, double* stats, int delta, int n_cu, QLayout* ql,
-                     const int* gate, hipStream_t s) {
+                     QEntry* queue, uint32_t* qcount, uint2* chg, uint32_t* chg_ctr, int delta, int n_cu,
+                     QLayout* ql, const int* gate, hipStream_t s) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
@@ -688,7 +762,7 @@ hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, cons
   const uint32_t seg = (uint32_t)(((ntiles + nw - 1) / nw) * 16);
   ql->seg = seg;
   ql->nwaves = (uint32_t)nw;
-  S1Args a{X, xnorm, g.n, g.k, g.d, seg, img, cn2o, cft, perm, cst, labels, queue, qcount, stats, gate};
+  S1Args a{X, xnorm, g.n, g.k, g.d, seg, img, cn2o, cft, perm, cst, labels, queue, qcount, chg, chg_ctr, gate};
   const size_t lds = (size_t)g.kp * g.dp * 2 + (size_t)nt * (g.dp + 4) * 4 + (size_t)g.kp * 4 + (size_t)nt * 4;
 #define KM_S1_CASE(NS2_, NB_)                                                                                   \
   case NS2_ * 100 + NB_:                                                                                        \
