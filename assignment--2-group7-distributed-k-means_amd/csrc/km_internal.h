@@ -235,15 +235,16 @@ hipError_t launch_s1_prep(const double* C64, const float* C32, const Geometry& g
                           uint4* img, float* cst, const int* gate, hipStream_t s);
 hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, const uint4* img, const float* cn2o,
                      const float* cft, const int32_t* perm, const float* cst, int32_t* labels,
-                     QEntry* queue, uint32_t* qcount, uint2* chg, uint32_t* chg_ctr, int delta, int n_cu,
+                     QEntry* queue, uint32_t* qcount, uint2* chg, uint32_t* chg_cnt, int delta, int n_cu,
                      QLayout* ql, const int* gate, hipStream_t s);
+// k_s1's change list: entries (wave segments) and per-wave counts to allocate
+size_t s1_chg_entries(const Geometry& g, int n_cu);
+size_t s1_wave_slots(int n_cu);
 // delta statistics: the change list of k_s1 into stats (deltas)
-hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_ctr,
+hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt,
                            double* stats, int n_cu, const int* gate, hipStream_t s);
-// delta statistics: mode 1 full += stats, stats = full; mode 0 full = stats;
-// chg_ctr (if given) is zeroed for the next change list
-hipError_t launch_s1_apply(double* stats, double* full, int64_t len, int mode, uint32_t* chg_ctr, const int* gate,
-                           hipStream_t s);
+// delta statistics: mode 1 full += stats, stats = full; mode 0 full = stats
+hipError_t launch_s1_apply(double* stats, double* full, int64_t len, int mode, const int* gate, hipStream_t s);
 hipError_t launch_gen_blobs(float* X, const Geometry& g, int64_t row_offset, int32_t n_centers, float box,
                             float stddev, uint64_t seed, hipStream_t s);
 

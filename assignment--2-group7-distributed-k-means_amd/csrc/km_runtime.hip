@@ -101,8 +101,8 @@ struct km_ctx {
   uint4* s1_img = nullptr;       // fragment-linear fp16 image of -2 s c
   float* s1_cst = nullptr;       // bound constants
   double* stats_full = nullptr;  // the full sums the deltas apply to
-  uint2* chg = nullptr;          // k_s1 change list (capacity n), {row, old << 16 | new}
-  uint32_t* chg_ctr = nullptr;   // its length (zeroed by km::launch_s1_apply)
+  uint2* chg = nullptr;          // k_s1 change list, one segment per wave, {row, old << 16 | new}
+  uint32_t* chg_cnt = nullptr;   // entries per wave segment (written by every delta k_s1)
   bool delta_ready = false;      // labels and stats_full describe one assignment
   int stats_pending = 0;         // the last assign left 0 nothing, 1 full sums, 2 deltas in stats
   float* bal = nullptr;  // fast screen: image error maxima (2 floats)
@@ -283,7 +283,7 @@ void free_centroids(km_ctx* c) {
   dfree(c->s1_cst);
   dfree(c->stats_full);
   dfree(c->chg);
-  dfree(c->chg_ctr);
+  dfree(c->chg_cnt);
   c->s1 = false;
   c->delta_ready = false;
   c->stats_pending = 0;
@@ -449,8 +449,8 @@ int apply_stats(km_ctx* c) {
   if (!c->s1) return KM_OK;
   const bool keep = kind == 2 || (kind == 1 && !c->want_sse);
   if (keep)
-    KM_HIP(km::launch_s1_apply(c->stats, c->stats_full, (int64_t)stats_len(c->g), kind == 2 ? 1 : 0, c->chg_ctr,
-                               c->gate, c->stream));
+    KM_HIP(km::launch_s1_apply(c->stats, c->stats_full, (int64_t)stats_len(c->g), kind == 2 ? 1 : 0, c->gate,
+                               c->stream));
   c->delta_ready = keep;
   return KM_OK;
 }
@@ -486,7 +486,7 @@ int run_assign(km_ctx* c, bool with_stats) {
     {
       ProfScope ps(c, KM_K_ASSIGN, true);
       KM_HIP(km::launch_s1(c->X, c->xnorm, g, c->s1_img, c->s1_cn2o, c->s1_cft, c->s1_perm, c->s1_cst,
-                           c->labels, c->queue, c->qcount, c->chg, c->chg_ctr, with_stats ? 1 : 0, c->n_cu,
+                           c->labels, c->queue, c->qcount, c->chg, c->chg_cnt, with_stats ? 1 : 0, c->n_cu,
                            &c->ql, c->gate, c->stream));
     }
     {
@@ -501,7 +501,7 @@ int run_assign(km_ctx* c, bool with_stats) {
     if (with_stats) {
       // the rows k_s1 moved between clusters (its change list) into the deltas
       ProfScope ps(c, KM_K_STATS);
-      KM_HIP(km::launch_s1_delta(c->X, g, c->chg, c->chg_ctr, c->stats, c->n_cu, c->gate, c->stream));
+      KM_HIP(km::launch_s1_delta(c->X, g, c->chg, c->chg_cnt, c->stats, c->n_cu, c->gate, c->stream));
     }
     c->stats_pending = with_stats ? 2 : 0;
     return KM_OK;
@@ -873,9 +873,8 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
       KM_HIP(hipMalloc(&c->s1_img, sizeof(_Float16) * kp * dp));
       KM_HIP(hipMalloc(&c->s1_cst, sizeof(float) * 8));
       KM_HIP(hipMalloc(&c->stats_full, sizeof(double) * stats_len(c->g)));
-      KM_HIP(hipMalloc(&c->chg, sizeof(uint2) * (size_t)std::max<int64_t>(c->g.n, 1)));
-      KM_HIP(hipMalloc(&c->chg_ctr, sizeof(uint32_t)));
-      KM_HIP(hipMemsetAsync(c->chg_ctr, 0, sizeof(uint32_t), c->stream));
+      KM_HIP(hipMalloc(&c->chg, sizeof(uint2) * km::s1_chg_entries(c->g, c->n_cu)));
+      KM_HIP(hipMalloc(&c->chg_cnt, sizeof(uint32_t) * km::s1_wave_slots(c->n_cu)));
     }
   }
   c->s1_recolor = true;

@@ -21,7 +21,9 @@
 //     other's MFMAs and loads;
 //   * statistics: either none (predict) or DELTAS -- a row whose label did not
 //     change since the last iteration adds nothing; a changed row is appended
-//     to a change list (row, old, new), and k_s1_delta moves its x from the
+//     to its wave's segment of a change list (row, old, new; no atomics: a
+//     wave's segment holds every row it can visit, the wave writes its count
+//     at the end), and k_s1_delta moves its x from the
 //     old cluster's float64 sums to the new one's through an LDS table per
 //     workgroup.  The runtime keeps the full sums (km_runtime.hip, "delta
 //     statistics"), so the sums the update reads are the reference's
@@ -263,8 +265,8 @@ struct S1Args {
   int32_t* labels;
   QEntry* queue;
   uint32_t* qcount;
-  uint2* chg;          // DELTA: changed rows {row, old << 16 | new}
-  uint32_t* chg_ctr;   // DELTA: entries in chg (zeroed by k_s1_apply)
+  uint2* chg;          // DELTA: changed rows {row, old << 16 | new}, [wave][seg]
+  uint32_t* chg_cnt;   // DELTA: entries per wave segment
   const int* gate;
 };
 
@@ -313,7 +315,8 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
   const uint32_t gw = blockIdx.x * S1_WAVES + wave;
   const uint32_t nw = gridDim.x * S1_WAVES;
   QEntry* wq = A.queue + (size_t)gw * A.seg;
-  uint32_t qn = 0, qf = 0;
+  uint2* wc = A.chg + (size_t)gw * A.seg;
+  uint32_t qn = 0, qf = 0, cc = 0;
   // chain id bits of this lane's 8 accumulator positions (cb, i): chain 16 cb + 4 q + i
   const uint32_t qbits = (uint32_t)(4 * q) << MB;
 
@@ -451,8 +454,12 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     const bool bad = !(m >= -3.0e38f && m <= 3.0e38f) || !(xn <= 3.0e38f);
     constexpr float RP = RHO * (1.0f + 2.0f * RHO);
     const float R = m + RP * fabsf(m) + 2.0f * E;
-    float T = R >= 0.0f ? R / (1.0f - RP) : R / (1.0f + RP);
-    T = T >= 0.0f ? T * (1.0f + 4.0f * U24) : T * (1.0f - 4.0f * U24);
+    // R / (1 -+ RP) by multiplication: the reciprocals rounded away from
+    // T's side by 2u, the products' roundings inside the final 4u
+    constexpr float IP = (1.0f / (1.0f - RP)) * (1.0f + 2.0f * U24);
+    constexpr float IM = (1.0f / (1.0f + RP)) * (1.0f - 2.0f * U24);
+    float T = R * (R >= 0.0f ? IP : IM);
+    T = T * (T >= 0.0f ? (1.0f + 4.0f * U24) : (1.0f - 4.0f * U24));
     const int32_t Tk = mono(f2u(T));
     // candidates: heads <= T (low 16 bits of the quad sum); chains whose
     // second key is <= T too (high 16 bits: the row goes to the full scan)
@@ -461,7 +468,7 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        cl += ((hk[cb][i] <= Tk) ? 1u : 0u) + ((mono(f2u(h2[cb][i])) <= Tk) ? 0x10000u : 0u);
+        cl += ((hk[cb][i] <= Tk) ? 1u : 0u) + ((h2[cb][i] <= T) ? 0x10000u : 0u);
     const uint32_t cq = bad ? 0u : quad_add_u(cl);
     const uint32_t cnt = cq & 0xFFFFu;
     const bool ovf = (cq >> 16) != 0u;
@@ -476,7 +483,11 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     if (__ballot(need) != 0ull) {
       // fp32 re-score of candidate slot sl: bounds of ||x - c|| (unscaled).
       // |Dt - D'| <= (FQ + 4) u D' <= 36 u D' (D' = ||x - c'||^2, FQ <= 32),
-      // then ||x - c|| = sqrt(D') +- g; sqrt and products: 8 u
+      // so sqrt(D') is within 18.1 u of sqrt(Dt); v_sqrt_f32 (within 2 ulp
+      // = 4 u taken here) gives r, sqrt(D') = r (1 +- 23 u), widened to
+      // 32 u; then ||x - c|| = sqrt(D') +- g, the fma and product: 4 u.
+      // Below 2^-96 the hardware sqrt loses accuracy: U takes sqrt(2^-96)
+      // (an over-estimate), L takes 0 (an under-estimate)
       auto partial = [&](uint32_t sl) {
         const float4* cp = reinterpret_cast<const float4*>(sCf + sl * CS + FQ * q);
         float acc = 0.0f;
@@ -496,8 +507,10 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
       // section 2: branchy running minima are miscompiled in divergent code
       // on this toolchain)
       auto take = [&](bool act, float Dt, uint32_t sl) {
-        const float U = (sqrtf(Dt * (1.0f + 48.0f * U24)) + gam) * (1.0f + 8.0f * U24);
-        const float L = (sqrtf(Dt * (1.0f - 48.0f * U24)) - gam) * (1.0f - 8.0f * U24);
+        const bool tiny = !(Dt >= 0x1p-96f);
+        const float r = __builtin_amdgcn_sqrtf(tiny ? 0x1p-96f : Dt);
+        const float U = fmaf(r, 1.0f + 32.0f * U24, gam) * (1.0f + 4.0f * U24);
+        const float L = fmaf(tiny ? 0.0f : r, 1.0f - 32.0f * U24, -gam) * (1.0f - 4.0f * U24);
         const bool w = act && U < U1;              // new winner
         const float Lc = w ? L1 : L;               // the displaced winner, or this one, joins the others
         const uint32_t sc = w ? s1 : sl;
@@ -555,14 +568,12 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
       const bool changed = decided && lab1 != old && q == 0;  // one lane per row
       const uint64_t mc = __ballot(changed);
       if (mc) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(A.chg_ctr, (uint32_t)__popcll(mc));
-        base = __shfl(base, 0);
         if (changed) {
           A.labels[row] = lab1;
-          A.chg[base + (uint32_t)__popcll(mc & ((1ull << lane) - 1ull))] =
+          wc[cc + (uint32_t)__popcll(mc & ((1ull << lane) - 1ull))] =
               make_uint2(row, ((uint32_t)old << 16) | (uint32_t)lab1);
         }
+        cc += (uint32_t)__popcll(mc);
       }
     }
     // queue: pair re-ranks from the front of the wave's segment, full scans
@@ -604,6 +615,7 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
   if (lane == 0) {
     A.qcount[2 * gw] = qn;
     A.qcount[2 * gw + 1] = qf;
+    if constexpr (MODE == 1) A.chg_cnt[gw] = cc;
   }
 }
 
@@ -612,11 +624,9 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
 // stats = full); mode 0 keeps an iteration's full statistics (full = stats),
 // the base of the next deltas.  The SSE slot rides along (0 in delta mode).
 __global__ __launch_bounds__(256) void k_s1_apply(double* __restrict__ stats, double* __restrict__ full, int64_t len,
-                                                  int mode, uint32_t* __restrict__ chg_ctr,
-                                                  const int* __restrict__ gate) {
+                                                  int mode, const int* __restrict__ gate) {
   if (*gate) return;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0 && chg_ctr) *chg_ctr = 0u;  // the change list is consumed (k_s1_delta ran before)
   if (i >= len) return;
   double v = stats[i];
   if (mode == 1) v = full[i] + v;
@@ -624,8 +634,10 @@ __global__ __launch_bounds__(256) void k_s1_apply(double* __restrict__ stats, do
   stats[i] = v;
 }
 
-// The change list of k_s1 into the delta statistics: each workgroup takes a
-// contiguous slice (at least S1D_MIN entries, so a short list wakes few
+// The change list of k_s1 into the delta statistics.  The list is nw wave
+// segments of seg entries, cnt[w] used in segment w; every workgroup scans
+// the counts (exclusive prefix in LDS), takes a contiguous slice of the
+// concatenated list (at least S1D_MIN entries, so a short list wakes few
 // workgroups and flushes few tables), moves each changed row's x from its
 // old cluster to its new one in an LDS float64 table [k][d+1] (lanes over
 // features: consecutive banks), 8 rows per wave in flight, then adds the
@@ -633,24 +645,53 @@ __global__ __launch_bounds__(256) void k_s1_apply(double* __restrict__ stats, do
 constexpr uint32_t S1D_MIN = 2048;
 constexpr int S1D_ROWS = 8;
 __global__ __launch_bounds__(1024) void k_s1_delta(const float* __restrict__ X, int dp, int d, int k,
-                                                   const uint2* __restrict__ chg,
-                                                   const uint32_t* __restrict__ chg_ctr, double* __restrict__ stats,
+                                                   const uint2* __restrict__ chg, const uint32_t* __restrict__ cnt,
+                                                   int nw, uint32_t seg, double* __restrict__ stats,
                                                    const int* __restrict__ gate) {
   if (*gate) return;
-  const uint32_t nc = *chg_ctr;
+  extern __shared__ double tab[];  // [k][d + 1], then pre[nw + 1]
+  const int d1 = d + 1;
+  uint32_t* pre = reinterpret_cast<uint32_t*>(tab + (size_t)k * d1);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  if (wave == 0) {
+    uint32_t run = 0;
+    for (int b = 0; b < nw; b += 64) {
+      const uint32_t v = b + lane < nw ? cnt[b + lane] : 0u;
+      uint32_t inc = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o);
+        inc += lane >= o ? t : 0u;
+      }
+      if (b + lane < nw) pre[b + lane] = run + inc - v;
+      run += __shfl(inc, 63);
+    }
+    if (lane == 0) pre[nw] = run;
+  }
+  __syncthreads();
+  const uint32_t nc = pre[nw];
   const uint32_t per = max(S1D_MIN, (nc + gridDim.x - 1u) / gridDim.x);
   const uint32_t e0 = blockIdx.x * per;
   if (e0 >= nc) return;
   const uint32_t e1 = min(nc, e0 + per);
-  extern __shared__ double tab[];  // [k][d + 1]
-  const int d1 = d + 1;
   for (int i = threadIdx.x; i < k * d1; i += blockDim.x) tab[i] = 0.0;
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  // entry e of the concatenation: segment w = the last with pre[w] <= e
+  auto at = [&](uint32_t e) {
+    int lo = 0, hi = nw - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    return chg[(size_t)lo * seg + (e - pre[lo])];
+  };
   for (uint32_t e = e0 + (uint32_t)wave * S1D_ROWS; e < e1; e += (uint32_t)nwv * S1D_ROWS) {
+    // lanes 0..7 locate the wave's 8 entries, then every lane takes them
+    uint2 mine = make_uint2(0u, 0u);
+    if (lane < S1D_ROWS) mine = at(min(e + (uint32_t)lane, e1 - 1u));
     uint2 c[S1D_ROWS];
 #pragma unroll
-    for (int r = 0; r < S1D_ROWS; ++r) c[r] = chg[min(e + (uint32_t)r, e1 - 1u)];
+    for (int r = 0; r < S1D_ROWS; ++r) c[r] = make_uint2(__shfl(mine.x, r), __shfl(mine.y, r));
     for (int f0 = 0; f0 < d; f0 += 64) {
       const int f = f0 + lane;
       float x[S1D_ROWS];
@@ -659,9 +700,9 @@ __global__ __launch_bounds__(1024) void k_s1_delta(const float* __restrict__ X, 
 #pragma unroll
       for (int r = 0; r < S1D_ROWS; ++r) {
         if (e + (uint32_t)r >= e1 || f >= d) continue;
-        const uint32_t old = c[r].y >> 16, nw = c[r].y & 0xFFFFu;
+        const uint32_t old = c[r].y >> 16, nw2 = c[r].y & 0xFFFFu;
         atomicAdd(tab + (size_t)old * d1 + f, -(double)x[r]);
-        atomicAdd(tab + (size_t)nw * d1 + f, (double)x[r]);
+        atomicAdd(tab + (size_t)nw2 * d1 + f, (double)x[r]);
       }
     }
     if (lane == 0)
@@ -682,20 +723,43 @@ __global__ __launch_bounds__(1024) void k_s1_delta(const float* __restrict__ X, 
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_ctr,
+// k_s1's grid: workgroups (one per CU at most, 8 waves each) and the rows
+// of one wave's queue / change-list segment
+static int64_t s1_grid(const Geometry& g, int n_cu, int* nbk, uint32_t* seg) {
+  const int64_t ntiles = (g.n + 15) / 16;
+  int64_t blocks = n_cu;
+  if (blocks > (ntiles + S1_WAVES - 1) / S1_WAVES) blocks = (ntiles + S1_WAVES - 1) / S1_WAVES;
+  *nbk = (int)blocks;
+  const int64_t nw = blocks * S1_WAVES;
+  *seg = nw ? (uint32_t)(((ntiles + nw - 1) / nw) * 16) : 0u;
+  return nw;
+}
+
+size_t s1_chg_entries(const Geometry& g, int n_cu) {
+  int nbk;
+  uint32_t seg;
+  const int64_t nw = s1_grid(g, n_cu, &nbk, &seg);
+  return (size_t)std::max<int64_t>(nw * (int64_t)seg, 1);
+}
+
+size_t s1_wave_slots(int n_cu) { return (size_t)n_cu * S1_WAVES; }
+
+hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt,
                            double* stats, int n_cu, const int* gate, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
-  const size_t lds = (size_t)g.k * (g.d + 1) * 8;
+  int nbk;
+  uint32_t seg;
+  const int64_t nw = s1_grid(g, n_cu, &nbk, &seg);
+  const size_t lds = (size_t)g.k * (g.d + 1) * 8 + (size_t)(nw + 1) * 4;
   if (lds > 160 * 1024 || g.k > 65535) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_s1_delta, dim3(n_cu), dim3(1024), lds, s, X, g.dp, g.d, g.k, chg, chg_ctr, stats, gate);
+  hipLaunchKernelGGL(k_s1_delta, dim3(n_cu), dim3(1024), lds, s, X, g.dp, g.d, g.k, chg, chg_cnt, (int)nw, seg, stats,
+                     gate);
   return hipGetLastError();
 }
 
-hipError_t launch_s1_apply(double* stats, double* full, int64_t len, int mode, uint32_t* chg_ctr, const int* gate,
-                           hipStream_t s) {
+hipError_t launch_s1_apply(double* stats, double* full, int64_t len, int mode, const int* gate, hipStream_t s) {
   if (len <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_s1_apply, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, stats, full, len, mode, chg_ctr,
-                     gate);
+  hipLaunchKernelGGL(k_s1_apply, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, stats, full, len, mode, gate);
   return hipGetLastError();
 }
 
@@ -747,22 +811,19 @@ hipError_t launch_s1_prep(const double* C64, const float* C32, const Geometry& g
 
 hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, const uint4* img, const float* cn2o,
                      const float* cft, const int32_t* perm, const float* cst, int32_t* labels,
-                     QEntry* queue, uint32_t* qcount, uint2* chg, uint32_t* chg_ctr, int delta, int n_cu,
+                     QEntry* queue, uint32_t* qcount, uint2* chg, uint32_t* chg_cnt, int delta, int n_cu,
                      QLayout* ql, const int* gate, hipStream_t s) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
   const S1Geo sg = s1_geo(g);
   const int nt = 32 << sg.mb;
-  const int64_t ntiles = (g.n + 15) / 16;
-  int64_t blocks = n_cu;
-  if (blocks > (ntiles + S1_WAVES - 1) / S1_WAVES) blocks = (ntiles + S1_WAVES - 1) / S1_WAVES;
-  const int nbk = (int)blocks;
-  const int64_t nw = (int64_t)nbk * S1_WAVES;
-  const uint32_t seg = (uint32_t)(((ntiles + nw - 1) / nw) * 16);
+  int nbk;
+  uint32_t seg;
+  const int64_t nw = s1_grid(g, n_cu, &nbk, &seg);
   ql->seg = seg;
   ql->nwaves = (uint32_t)nw;
-  S1Args a{X, xnorm, g.n, g.k, g.d, seg, img, cn2o, cft, perm, cst, labels, queue, qcount, chg, chg_ctr, gate};
+  S1Args a{X, xnorm, g.n, g.k, g.d, seg, img, cn2o, cft, perm, cst, labels, queue, qcount, chg, chg_cnt, gate};
   const size_t lds = (size_t)g.kp * g.dp * 2 + (size_t)nt * (g.dp + 4) * 4 + (size_t)g.kp * 4 + (size_t)nt * 4;
 #define KM_S1_CASE(NS2_, NB_)                                                                                   \
   case NS2_ * 100 + NB_:                                                                                        \

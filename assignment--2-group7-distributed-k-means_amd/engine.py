@@ -46,6 +46,7 @@ class HipEngine:
         self.k = 0
         self._stats_t = None
         self._tstream = None
+        self._coll_ev = None        # [(start, end)] HIP events around each collective while timed
         self.distributed = distributed
         if distributed:
             import torch
@@ -100,13 +101,14 @@ class HipEngine:
 
     def set_screen(self, mode: int) -> None:
         """Screening kernel of the fused path (-1 auto; 0 fp16x3; 1 fp16x3 +
-        per-key bounds; 2 / 3 the fast fp16 screen, diagnostic library only).
-        A cost choice only: results are exact in every mode (tests pin each
-        one)."""
+        per-key bounds; 2 / 3 the fast fp16 screen, diagnostic library only;
+        4 k_s1, one fp16 MFMA per product with in-kernel fp32 re-scoring and
+        delta statistics, where the geometry has it).  A cost choice only:
+        results are exact in every mode (tests pin each one)."""
         self._c(self.lib.km_set_screen(self.ctx, int(mode)), "km_set_screen")
 
     def screen(self) -> int:
-        """The screen the next fused launch uses (0..3)."""
+        """The screen the next fused launch uses (0..4)."""
         m = ctypes.c_int32()
         self._c(self.lib.km_get_screen(self.ctx, ctypes.byref(m)), "km_get_screen")
         return m.value
@@ -147,9 +149,29 @@ class HipEngine:
         km_update_async enqueued next on the engine stream read the summed
         buffer.  gloo (CPU tensors) completes inside wait()."""
         with self._torch.cuda.stream(self._tstream):
+            if self._coll_ev is not None:
+                e0 = self._torch.cuda.Event(enable_timing=True)
+                e1 = self._torch.cuda.Event(enable_timing=True)
+                e0.record(self._tstream)
             work = fn(self._stats_t if tensor is None else tensor, async_op=True)
             if work is not None:
                 work.wait()
+            if self._coll_ev is not None:
+                e1.record(self._tstream)
+                self._coll_ev.append((e0, e1))
+
+    def time_collectives(self, enable: bool) -> None:
+        """Record HIP events on the engine stream around each collective
+        (from the statistics being ready to the summed buffer being usable by
+        the next kernel); read with ``collective_ms``."""
+        self._coll_ev = [] if enable else None
+
+    def collective_ms(self) -> Tuple[float, int]:
+        """(total ms, collectives) recorded since ``time_collectives(True)``."""
+        evs = self._coll_ev or []
+        if evs:
+            self._torch.cuda.synchronize(self.device)
+        return sum(a.elapsed_time(b) for a, b in evs), len(evs)
 
     def update(self) -> Tuple[_lib.KmStatus, np.ndarray]:
         st = _lib.KmStatus()
@@ -248,6 +270,10 @@ class HipEngine:
         out = np.empty(self.n, dtype=np.int32)
         self._c(self.lib.km_predict(self.ctx, _ptr(out, _PI32)), "km_predict")
         return out
+
+    def predict_device(self) -> None:
+        """km_predict with the labels left in HBM (no host copy)."""
+        self._c(self.lib.km_predict(self.ctx, None), "km_predict")
 
     def labels(self) -> np.ndarray:
         out = np.empty(self.n, dtype=np.int32)

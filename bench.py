@@ -63,6 +63,9 @@ def parse():
     p.add_argument("--sse", type=int, default=None, choices=[0, 1],
                    help="compute_sse (kmeans_spark.py:38); default: on for c4, whose BASELINE config "
                         "(configs[3]) states compute_sse=True, off elsewhere (the reference default)")
+    p.add_argument("--predict", type=int, default=0, metavar="P",
+                   help="after the fit steps, time P predict passes (km_predict, labels left in HBM; "
+                        "kmeans_spark.py:321-352) and add a 'predict' object to the line")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work per worker")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="per-launch HBM bytes from a rocprofv3 --pmc pass (optional)")
@@ -189,9 +192,13 @@ def main():
     # point), empties or NaN; the rate counts what ran, never args.steps
     ran = run.iterations_ran - ran0
     eng.profile(True, phases=("resolve", "update", "prep"), every=1)
+    if world > 1:
+        eng.time_collectives(True)   # HIP events around each all-reduce, engine stream
     run.run(km, log, args.warmup + args.steps + 2, first=args.warmup + args.steps)
     eng.sync()
     eng.profile(False)
+    coll = eng.collective_ms() if world > 1 else None
+    eng.time_collectives(False)
     dt = float(comm.allreduce_np(np.array([t1 - t0])).max()) if world == 1 else None
     if world > 1:
         import torch.distributed as dist
@@ -262,7 +269,8 @@ def main():
         kname = (("k_fused16 (fp16x3 screen on 16x16x32 MFMA + f64 sums)" if info["dp"] % 32 == 0 else
                   "k_fused (fp16x3 screen on 32x32x16 MFMA + f64 sums)") if info["fused_stats"] else
                  "k_assign_wide (fp16x3 screen, feature chunks)" if info["dp"] > 256 else
-                 "k_assign_mfma (fp16x3 screen)")
+                 "k_assign_mfma16 (fp16x3 screen on 16x16x32 MFMA)" if info["dp"] % 32 == 0 else
+                 "k_assign_mfma (fp16x3 screen on 32x32x16 MFMA)")
         roof = {"bound": "mfma", "achieved": ach, "peak": F16X3_EFFECTIVE_TFLOPS, "unit": "TFLOP/s",
                 "frac": ach / F16X3_EFFECTIVE_TFLOPS, "traffic": traffic, "kernel": kname,
                 "peak_note": "dense f16 MFMA 2516.6 TF / 3 (fp16x3 split: 3 MFMAs per product); "
@@ -275,6 +283,38 @@ def main():
                 "traffic": traffic, "kernel": "k_stats" if dom == "stats" else "k_assign_small",
                 "bytes_note": "N*(d*4+4) per launch (rows once + labels)"}
     kernel_ms = {kk: (v[0] / max(v[1], 1)) for kk, v in kern.items()}
+    if kern["update"][1] == 0 and kern["assign"][1] > 0:
+        # the single-rank small path folds the update into the assign launch
+        # (k_assign_small's last workgroup): one launch carries both
+        kernel_ms["assign+update (folded)"] = kernel_ms.pop("assign")
+        kernel_ms.pop("update")
+    if coll is not None:
+        kernel_ms["allreduce"] = coll[0] / max(coll[1], 1)
+    pred = None
+    if args.predict > 0:
+        # predict (kmeans_spark.py:321-352): one assignment pass with no
+        # statistics; labels stay in HBM (the LabelsRDD the caller collects)
+        eng.profile(True, phases=("assign", "resolve"), every=1)
+        eng.predict_device()                    # one untimed pass
+        eng.prof_read("assign"), eng.prof_read("resolve")
+        comm.barrier()
+        tp0 = time.perf_counter()
+        for _ in range(args.predict):
+            eng.predict_device()                # synchronises per pass
+        tp1 = time.perf_counter()
+        pa, pr = eng.prof_read("assign"), eng.prof_read("resolve")
+        eng.profile(False)
+        ms_a = pa[0] / max(pa[1], 1)
+        ms_w = (tp1 - tp0) / args.predict * 1e3
+        pred = {"passes": args.predict, "ms_per_pass": ms_w, "kernel_ms": {"assign": ms_a, "resolve": pr[0] / max(pr[1], 1)},
+                "gb_s": n_local * d * 4 / (ms_a / 1e3) / 1e9, "points_per_sec": n_local / (ms_w / 1e3),
+                "kernel": ("k_assign_small (labels only)" if info["path"] == 1 else
+                           "k_s1 (labels only)" if screen == 4 else
+                           "k_fused16 / k_fused (no statistics)" if info["fused_stats"] else
+                           "k_assign_wide" if info["dp"] > 256 else
+                           "k_assign_mfma16" if info["dp"] % 32 == 0 else "k_assign_mfma"),
+                "note": "ms_per_pass: host wall time per km_predict (launch + sync, labels left in HBM); "
+                        "gb_s: rows read once (N*d*4) / HIP-event time of the assign launch"}
 
     if rank == 0:
         it_s = ran / dt
@@ -291,6 +331,7 @@ def main():
             "resolve": {"q_rerank": run.last["q_rerank"], "q_full": run.last["q_full"]} if run.last else None,
             "empty_repairs_on_device": run.device_repairs,
             "screen": screen,
+            "predict": pred,
             "arith": ("fp16 MFMA screen (balanced image, pairwise bound)" if screen in (2, 3) else
                       "one fp16 MFMA per product, candidates re-scored in fp32 with a rigorous bound, float64 "
                       "delta statistics" if screen == 4 else

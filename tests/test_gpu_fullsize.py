@@ -109,3 +109,46 @@ def test_full_size_c5_poor_seeds_device_repair():
     np.testing.assert_array_equal(C1[empty], run.rows(gidx[:len(empty)]))
     full = np.nonzero(counts > 0)[0]
     assert np.all(np.isfinite(C1[full])) and np.all(np.abs(C1[full]) < 20)
+
+
+def test_full_size_c2_through_lloyd_runner():
+    # c2 (10M x 16, k 8) through LloydRunner.run on one rank: the small path's
+    # one-launch iteration (k_assign_small with the update folded into its
+    # last workgroup, which takes the queued rows over from the others) at
+    # full size.  Iterations 1-2, then 3 alone, so the centroids the third
+    # assignment used are known: counts, checksum of checksums and sampled
+    # labels of that assignment (kmeans_spark.py:147-206).
+    import kmeans_amd
+    from kmeans_amd.comm import Communicator
+
+    N, d, k = 10_000_000, 16, 8
+    km = kmeans_amd.KMeans(k=k, max_iter=10, tolerance=1e-300, seed=42)
+    km.verbose = False
+    data = kmeans_amd.DeviceBlobs(n=N, d=d, n_centers=k, box=10.0, std=1.0, seed=2024)
+    run = km._make_runner(data, Communicator())
+    eng = run.engine
+    eng.set_centroids(km._initialize_centroids(run))
+    assert eng.info()["path"] == 1
+    sx = eng.sum_x()
+    run.run(km, None, 2)
+    assert run.iterations_ran == 2
+    C_prev = eng.get_centroids(0)
+    run.run(km, None, 3, first=2)
+    assert run.iterations_ran == 3
+    counts = np.asarray(run.last["counts"])
+    C3 = eng.get_centroids(0)
+    labels = eng.labels()
+    assert int(counts.sum()) == N
+    np.testing.assert_array_equal(np.bincount(labels, minlength=k), counts)
+    nz = counts > 0
+    tot = (counts[nz, None].astype(np.float64) * C3[nz]).sum(axis=0)
+    np.testing.assert_allclose(tot, sx, rtol=1e-9, atol=1e-4)
+    gidx = np.sort(np.random.default_rng(11).choice(N, 20000, replace=False))
+    Xs = np.asarray(run.rows(gidx.tolist()), dtype=np.float64)
+    lab_ref, _, _ = orc.assign(Xs, C_prev)
+    np.testing.assert_array_equal(labels[gidx], lab_ref)
+    # the update of the same launch: the new centroids are the sampled
+    # clusters' means to within the sample's noise, and exactly the folded
+    # sums over the counts (checked above); predict with them is stable
+    pred = eng.predict()
+    np.testing.assert_array_equal(pred[gidx], orc.assign(Xs, C3)[0])
