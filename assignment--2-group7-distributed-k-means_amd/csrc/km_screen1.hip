@@ -66,6 +66,11 @@ constexpr float U24 = 5.9604644775390625e-08f;  // 2^-24
 constexpr float U16 = 4.8828125e-04f;           // 2^-11, fp16 unit roundoff
 constexpr int S1_WAVES = 8;                     // 512 threads: two waves per SIMD
 constexpr int S1_LMAX = 4;                      // candidates re-scored per row
+constexpr int S1_RING = 16;                     // rows per re-scoring batch (one per quad of a wave)
+
+// the re-scoring batches run where a wave's ring (S1_RING rows of DP floats
+// + 16 B) fits beside the tables: dp <= 64
+constexpr bool s1_batched(int ns2) { return ns2 <= 2; }
 
 constexpr int ceil_log2_c(int v) { return v <= 1 ? 0 : 1 + ceil_log2_c((v + 1) / 2); }
 
@@ -292,6 +297,11 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
   float* sCf = reinterpret_cast<float*>(smem + KP * DP * 2);  // [NT][CS]
   float* sCn = sCf + NT * CS;                                 // [KP] output order
   int32_t* sPerm = reinterpret_cast<int32_t*>(sCn + KP);      // [NT]
+  // per wave: the re-scoring ring, rows' x [S1_RING][DP] and {row, old | cnt
+  // << 16, s0 | s1 << 16, s2 | s3 << 16}
+  constexpr bool BATCH = s1_batched(NS2);
+  float* sRx = reinterpret_cast<float*>(sPerm + NT);                   // [S1_WAVES][S1_RING][DP]
+  uint4* sRm = reinterpret_cast<uint4*>(sRx + S1_WAVES * S1_RING * DP);  // [S1_WAVES][S1_RING]
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -333,6 +343,148 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     for (int u = 0; u < FQ / 4; ++u) B.x[u] = xr[u];
     B.xn = A.xnorm[rr];
     if constexpr (MODE == 1) B.old = A.labels[rr];
+  };
+
+  // fp32 re-score of candidates (slots sl[0..cnt-1], ascending key order)
+  // from the fp32 table: the winner by the smallest upper bound, decided when
+  // every other candidate's lower bound is above it; a near tie of exactly
+  // two candidates goes to the float64 pair re-rank (kind 1), anything else
+  // to the full scan (kind 2).  Bounds of ||x - c|| (unscaled):
+  // |Dt - D'| <= (FQ + 4) u D' <= 36 u D' (D' = ||x - c'||^2, FQ <= 32), so
+  // sqrt(D') is within 18.1 u of sqrt(Dt); v_sqrt_f32 (within 2 ulp = 4 u
+  // taken here) gives r, sqrt(D') = r (1 +- 23 u), widened to 32 u; then
+  // ||x - c|| = sqrt(D') +- g, the fma and product: 4 u.  Below 2^-96 the
+  // hardware sqrt loses accuracy: U takes sqrt(2^-96) (an over-estimate), L
+  // takes 0 (an under-estimate)
+  auto decide = [&](bool act0, uint32_t cnt, const uint32_t* sl, const float4* xv, int32_t& lab1, int32_t& lab2,
+                    uint32_t& kind) {
+    auto partial = [&](uint32_t slot) {
+      const float4* cp = reinterpret_cast<const float4*>(sCf + slot * CS + FQ * q);
+      float acc = 0.0f;
+#pragma unroll
+      for (int u = 0; u < FQ / 4; ++u) {
+        const float4 c = cp[u];
+        const float4 x = xv[u];
+        const float d0 = x.x - c.x, d1 = x.y - c.y, d2 = x.z - c.z, d3 = x.w - c.w;
+        acc = fmaf(d0, d0, acc);
+        acc = fmaf(d1, d1, acc);
+        acc = fmaf(d2, d2, acc);
+        acc = fmaf(d3, d3, acc);
+      }
+      return acc;
+    };
+    // winner (smallest upper bound U1, its lower bound L1, slot s1) and the
+    // smallest lower bound of the others (Lo, slot s2), select form
+    // throughout (branchy running minima are
+    // miscompiled in divergent code on this toolchain)
+    uint32_t s1 = sl[0], s2 = sl[0];
+    float U1 = FLT_MAX, L1 = FLT_MAX, Lo = FLT_MAX;
+    auto take = [&](bool act, float Dt, uint32_t slot) {
+      const bool tiny = !(Dt >= 0x1p-96f);
+      const float r = __builtin_amdgcn_sqrtf(tiny ? 0x1p-96f : Dt);
+      const float U = fmaf(r, 1.0f + 32.0f * U24, gam) * (1.0f + 4.0f * U24);
+      const float L = fmaf(tiny ? 0.0f : r, 1.0f - 32.0f * U24, -gam) * (1.0f - 4.0f * U24);
+      const bool w = act && U < U1;              // new winner
+      const float Lc = w ? L1 : L;               // the displaced winner, or this one, joins the others
+      const uint32_t sc = w ? s1 : slot;
+      const bool lo = act && Lc < Lo;
+      Lo = lo ? Lc : Lo;
+      s2 = lo ? sc : s2;
+      U1 = w ? U : U1;
+      L1 = w ? L : L1;
+      s1 = w ? slot : s1;
+    };
+    // the first two (every row here has them) in one round: both tables'
+    // reads in flight together; inactive lanes read slot 0 and ignore it
+    {
+      const uint32_t sa = act0 ? sl[0] : 0u, sb = act0 ? sl[1] : 0u;
+      const float pa = partial(sa), pb = partial(sb);
+      take(act0, quad_sum(pa), sa);
+      take(act0, quad_sum(pb), sb);
+    }
+#pragma unroll
+    for (int r = 2; r < S1_LMAX; ++r) {
+      const bool act = act0 && (uint32_t)r < cnt;
+      if (__ballot(act) == 0ull) break;
+      const uint32_t slot = act ? sl[r] : 0u;
+      take(act, quad_sum(partial(slot)), slot);
+    }
+    const int32_t l1 = sPerm[s1], l2 = sPerm[s2];
+    uint32_t kd = 2u;
+    if (l1 >= 0) {
+      if (Lo > U1)
+        kd = 0u;
+      else if (cnt == 2u && l2 >= 0)
+        kd = 1u;
+    }
+    if (act0) {
+      lab1 = l1;
+      lab2 = l2;
+      kind = kd;
+    }
+  };
+  // a row's outcome (every lane of its quad calls with the same values):
+  // decided (kind 0) -> its label (MODE 1: only a changed one, appended to
+  // the wave's change list); kind 1 / 2 -> the queue, pair re-ranks from the
+  // front of the wave's segment, full scans from the back (k_fused16's
+  // layout, read by launch_resolve)
+  auto emit = [&](bool act, uint32_t row, uint32_t kind, int32_t lab1, int32_t lab2, int32_t old) {
+    const bool decided = act && kind == 0u;
+    if constexpr (MODE == 0) {
+      (void)old;
+      if (decided && q == 0) A.labels[row] = lab1;
+    } else {
+      const bool changed = decided && lab1 != old && q == 0;  // one lane per row
+      const uint64_t mc = __ballot(changed);
+      if (mc) {
+        if (changed) {
+          A.labels[row] = lab1;
+          wc[cc + (uint32_t)__popcll(mc & ((1ull << lane) - 1ull))] =
+              make_uint2(row, ((uint32_t)old << 16) | (uint32_t)lab1);
+        }
+        cc += (uint32_t)__popcll(mc);
+      }
+    }
+    const bool enq = act && kind != 0u && q == 0;
+    const uint64_t mq = __ballot(enq);
+    if (mq) {
+      const uint64_t m1 = __ballot(enq && kind == 1u);
+      const uint64_t m2 = mq & ~m1;
+      const uint64_t below = (1ull << lane) - 1ull;
+      if (enq) {
+        QEntry qe;
+        qe.row = row;
+        qe.i1 = kind == 1u ? (uint32_t)lab1 : 0u;
+        qe.i2 = kind == 1u ? (uint32_t)lab2 : 0u;
+        qe.kind = kind;
+        const uint32_t pos = (kind == 1u) ? qn + (uint32_t)__popcll(m1 & below)
+                                          : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
+        wq[pos] = qe;
+      }
+      qn += (uint32_t)__popcll(m1);
+      qf += (uint32_t)__popcll(m2);
+    }
+  };
+  // the first nb rows of the wave's ring, one per quad: re-scored, emitted
+  uint32_t rc = 0;  // rows in the ring (< S1_RING between tiles)
+  auto rescore = [&](uint32_t nb) {
+    if constexpr (BATCH) {
+      const bool act = (uint32_t)c16 < nb;
+      const uint32_t slot = act ? (uint32_t)c16 : 0u;
+      const uint4 mt = sRm[wave * S1_RING + slot];
+      float4 xv[FQ / 4];
+      const float4* xs = reinterpret_cast<const float4*>(sRx + (wave * S1_RING + slot) * DP + FQ * q);
+#pragma unroll
+      for (int u = 0; u < FQ / 4; ++u) xv[u] = xs[u];
+      const uint32_t cnt = mt.y >> 16;
+      const uint32_t sl[4] = {mt.z & 0xFFFFu, mt.z >> 16, mt.w & 0xFFFFu, mt.w >> 16};
+      int32_t lab1 = 0, lab2 = 0;
+      uint32_t kind = 2u;
+      decide(act, cnt, sl, xv, lab1, lab2, kind);
+      emit(act, mt.x, kind, lab1, lab2, (int32_t)(mt.y & 0xFFFFu));
+    } else {
+      (void)nb;
+    }
   };
 
   auto process = [&](uint32_t tile, const Buf& B) {
@@ -473,129 +625,79 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     const uint32_t cnt = cq & 0xFFFFu;
     const bool ovf = (cq >> 16) != 0u;
 
-    // re-scored rows: the winner (smallest upper bound U1, its lower bound
-    // L1, slot s1) and the smallest lower bound of the other candidates (Lo,
-    // slot s2)
     const uint32_t sm = unmono(mki) & SLOTM;
-    uint32_t s1 = sm, s2 = sm;
-    float U1 = FLT_MAX, L1 = FLT_MAX, Lo = FLT_MAX;
-    const bool need = valid && !bad && !ovf && cnt >= 2u && cnt <= (uint32_t)S1_LMAX;
-    if (__ballot(need) != 0ull) {
-      // fp32 re-score of candidate slot sl: bounds of ||x - c|| (unscaled).
-      // |Dt - D'| <= (FQ + 4) u D' <= 36 u D' (D' = ||x - c'||^2, FQ <= 32),
-      // so sqrt(D') is within 18.1 u of sqrt(Dt); v_sqrt_f32 (within 2 ulp
-      // = 4 u taken here) gives r, sqrt(D') = r (1 +- 23 u), widened to
-      // 32 u; then ||x - c|| = sqrt(D') +- g, the fma and product: 4 u.
-      // Below 2^-96 the hardware sqrt loses accuracy: U takes sqrt(2^-96)
-      // (an over-estimate), L takes 0 (an under-estimate)
-      auto partial = [&](uint32_t sl) {
-        const float4* cp = reinterpret_cast<const float4*>(sCf + sl * CS + FQ * q);
-        float acc = 0.0f;
+    const bool ok = valid && !bad && !ovf;
+    const bool needy = ok && cnt >= 2u && cnt <= (uint32_t)S1_LMAX;
+    const int32_t labm = sPerm[sm];
+    // one candidate: the screen decides; none / too many / an open chain /
+    // non-finite input: the full scan (kind 2)
+    const bool dec1 = ok && cnt == 1u && labm >= 0;
+    int32_t old = 0;
+    if constexpr (MODE == 1) old = (int32_t)min((uint32_t)B.old, (uint32_t)(A.k - 1));
+    if constexpr (BATCH) {
+      emit(valid && !needy, row, dec1 ? 0u : 2u, labm, 0, old);
+      // rows with 2..LMAX candidates: into the wave's ring with their
+      // candidates in ascending key order (the first two are the row's two
+      // smallest heads); a full ring is re-scored as one batch
+      const uint64_t mrow = __ballot(needy && q == 0);
+      if (mrow) {
+        uint32_t s2c = 0, s3c = 0;
+        if (__ballot(needy && cnt >= 3u) != 0ull) {
+          int32_t prev = lb;
 #pragma unroll
-        for (int u = 0; u < FQ / 4; ++u) {
-          const float4 c = cp[u];
-          const float4 x = B.x[u];
-          const float d0 = x.x - c.x, d1 = x.y - c.y, d2 = x.z - c.z, d3 = x.w - c.w;
-          acc = fmaf(d0, d0, acc);
-          acc = fmaf(d1, d1, acc);
-          acc = fmaf(d2, d2, acc);
-          acc = fmaf(d3, d3, acc);
+          for (int r = 2; r < S1_LMAX; ++r) {
+            int32_t nl = INT32_MAX;
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) nl = min(nl, hk[cb][i] > prev ? hk[cb][i] : INT32_MAX);
+            prev = quad_min_i(nl);
+            const uint32_t sl = (uint32_t)r < cnt ? (unmono(prev) & SLOTM) : 0u;
+            if (r == 2) s2c = sl; else s3c = sl;
+          }
         }
-        return acc;
-      };
-      // winner / others bookkeeping, select form throughout (DESIGN.md
-      // section 2: branchy running minima are miscompiled in divergent code
-      // on this toolchain)
-      auto take = [&](bool act, float Dt, uint32_t sl) {
-        const bool tiny = !(Dt >= 0x1p-96f);
-        const float r = __builtin_amdgcn_sqrtf(tiny ? 0x1p-96f : Dt);
-        const float U = fmaf(r, 1.0f + 32.0f * U24, gam) * (1.0f + 4.0f * U24);
-        const float L = fmaf(tiny ? 0.0f : r, 1.0f - 32.0f * U24, -gam) * (1.0f - 4.0f * U24);
-        const bool w = act && U < U1;              // new winner
-        const float Lc = w ? L1 : L;               // the displaced winner, or this one, joins the others
-        const uint32_t sc = w ? s1 : sl;
-        const bool lo = act && Lc < Lo;
-        Lo = lo ? Lc : Lo;
-        s2 = lo ? sc : s2;
-        U1 = w ? U : U1;
-        L1 = w ? L : L1;
-        s1 = w ? sl : s1;
-      };
-      // the first two candidates (every needy row has them) in one round:
-      // both tables' reads in flight together; rows without a need score
-      // slot 0 and ignore it
-      {
-        const uint32_t sa = need ? (unmono(mki) & SLOTM) : 0u;
-        const uint32_t sb = need ? (unmono(lb) & SLOTM) : 0u;
-        const float pa = partial(sa), pb = partial(sb);
-        take(need, quad_sum(pa), sa);
-        take(need, quad_sum(pb), sb);
+        const uint32_t nn = (uint32_t)__popcll(mrow);
+        const uint32_t rk = (uint32_t)__popcll(mrow & ((1ull << c16) - 1ull));
+        const uint32_t space = (uint32_t)S1_RING - rc;
+        const uint4 meta = make_uint4(row, (uint32_t)old | (cnt << 16), sm | ((unmono(lb) & SLOTM) << 16),
+                                      s2c | (s3c << 16));
+        auto stash = [&](uint32_t slot) {
+          float4* xs = reinterpret_cast<float4*>(sRx + (wave * S1_RING + slot) * DP + FQ * q);
+#pragma unroll
+          for (int u = 0; u < FQ / 4; ++u) xs[u] = B.x[u];
+          if (q == 0) sRm[wave * S1_RING + slot] = meta;
+        };
+        if (needy && rk < space) stash(rc + rk);
+        if (nn >= space) {
+          rescore((uint32_t)S1_RING);
+          if (needy && rk >= space) stash(rk - space);
+          rc = nn - space;
+        } else {
+          rc += nn;
+        }
       }
-      // the rest in ascending key order: the smallest head above the last
+    } else {
+      // dp > 64: the candidates re-scored in the tile, every row of it
+      uint32_t sl[S1_LMAX];
+      sl[0] = sm;
+      sl[1] = unmono(lb) & SLOTM;
       int32_t prev = lb;
-#pragma unroll 1
+#pragma unroll
       for (int r = 2; r < S1_LMAX; ++r) {
-        const bool act = need && (uint32_t)r < cnt;
-        if (__ballot(act) == 0ull) break;
+        sl[r] = 0u;
+        if (__ballot(needy && (uint32_t)r < cnt) == 0ull) continue;
         int32_t nl = INT32_MAX;
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int i = 0; i < 4; ++i) nl = min(nl, hk[cb][i] > prev ? hk[cb][i] : INT32_MAX);
-        const int32_t cur = quad_min_i(nl);
-        prev = cur;
-        const uint32_t sl = act ? (unmono(cur) & SLOTM) : 0u;
-        take(act, quad_sum(partial(sl)), sl);
+        prev = quad_min_i(nl);
+        sl[r] = unmono(prev) & SLOTM;
       }
-    }
-    // decision: 0 decided, 1 pair re-rank (k_rerank2), 2 full scan (k_fullscan)
-    const int32_t lab1 = sPerm[s1];
-    const int32_t lab2 = sPerm[s2];
-    uint32_t kind = 2u;
-    if (!bad && !ovf && cnt >= 1u && cnt <= (uint32_t)S1_LMAX && lab1 >= 0) {
-      if (cnt == 1u || Lo > U1)
-        kind = 0u;
-      else if (cnt == 2u && lab2 >= 0)
-        kind = 1u;
-    }
-    const bool decided = valid && kind == 0u;
-    if constexpr (MODE == 0) {
-      if (decided && q == 0) A.labels[row] = lab1;
-    } else {
-      // (a previous label is always a cluster index; clamped so that a
-      // corrupt one can never address outside the sums)
-      const int32_t old = (int32_t)min((uint32_t)B.old, (uint32_t)(A.k - 1));
-      const bool changed = decided && lab1 != old && q == 0;  // one lane per row
-      const uint64_t mc = __ballot(changed);
-      if (mc) {
-        if (changed) {
-          A.labels[row] = lab1;
-          wc[cc + (uint32_t)__popcll(mc & ((1ull << lane) - 1ull))] =
-              make_uint2(row, ((uint32_t)old << 16) | (uint32_t)lab1);
-        }
-        cc += (uint32_t)__popcll(mc);
-      }
-    }
-    // queue: pair re-ranks from the front of the wave's segment, full scans
-    // from the back (k_fused16's layout, read by launch_resolve)
-    const bool enq = valid && kind != 0u && q == 0;
-    const uint64_t mq = __ballot(enq);
-    if (mq) {
-      const uint64_t m1 = __ballot(enq && kind == 1u);
-      const uint64_t m2 = mq & ~m1;
-      const uint64_t below = (1ull << lane) - 1ull;
-      if (enq) {
-        QEntry qe;
-        qe.row = (uint32_t)row;
-        qe.i1 = kind == 1u ? (uint32_t)lab1 : 0u;
-        qe.i2 = kind == 1u ? (uint32_t)lab2 : 0u;
-        qe.kind = kind;
-        const uint32_t pos = (kind == 1u) ? qn + (uint32_t)__popcll(m1 & below)
-                                          : A.seg - 1u - (qf + (uint32_t)__popcll(m2 & below));
-        wq[pos] = qe;
-      }
-      qn += (uint32_t)__popcll(m1);
-      qf += (uint32_t)__popcll(m2);
+      int32_t lab1 = labm, lab2 = 0;
+      uint32_t kind = dec1 ? 0u : 2u;
+      if (__ballot(needy) != 0ull) decide(needy, cnt, sl, B.x, lab1, lab2, kind);
+      emit(valid, row, kind, lab1, lab2, old);
     }
   };
 
@@ -612,6 +714,7 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     load(tile + 2 * nw, b0);
     process(tile + nw, b1);
   }
+  if (rc) rescore(rc);
   if (lane == 0) {
     A.qcount[2 * gw] = qn;
     A.qcount[2 * gw + 1] = qf;
@@ -769,7 +872,7 @@ bool s1_ok(const Geometry& g) {
   if (g.dp % 32 || g.kp % 64) return false;
   switch ((g.dp / 32) * 100 + g.kp / 32) {
     case 202: case 204: case 206: case 208:
-    case 102: case 104: case 106: case 108: case 112: case 116:
+    case 102: case 104: case 106: case 108:
     case 402: case 404:
       return true;
     default:
@@ -824,7 +927,9 @@ hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, cons
   ql->seg = seg;
   ql->nwaves = (uint32_t)nw;
   S1Args a{X, xnorm, g.n, g.k, g.d, seg, img, cn2o, cft, perm, cst, labels, queue, qcount, chg, chg_cnt, gate};
-  const size_t lds = (size_t)g.kp * g.dp * 2 + (size_t)nt * (g.dp + 4) * 4 + (size_t)g.kp * 4 + (size_t)nt * 4;
+  const size_t lds = (size_t)g.kp * g.dp * 2 + (size_t)nt * (g.dp + 4) * 4 + (size_t)g.kp * 4 + (size_t)nt * 4 +
+                     (s1_batched(sg.ns2) ? (size_t)S1_WAVES * S1_RING * (g.dp * 4 + 16) : 0);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
 #define KM_S1_CASE(NS2_, NB_)                                                                                   \
   case NS2_ * 100 + NB_:                                                                                        \
     if (delta)                                                                                                  \
@@ -834,7 +939,7 @@ hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, cons
     break;
   switch (sg.ns2 * 100 + sg.nb) {
     KM_S1_CASE(2, 2) KM_S1_CASE(2, 4) KM_S1_CASE(2, 6) KM_S1_CASE(2, 8)
-    KM_S1_CASE(1, 2) KM_S1_CASE(1, 4) KM_S1_CASE(1, 6) KM_S1_CASE(1, 8) KM_S1_CASE(1, 12) KM_S1_CASE(1, 16)
+    KM_S1_CASE(1, 2) KM_S1_CASE(1, 4) KM_S1_CASE(1, 6) KM_S1_CASE(1, 8)
     KM_S1_CASE(4, 2) KM_S1_CASE(4, 4)
     default:
       return hipErrorInvalidValue;

@@ -1,6 +1,6 @@
 """profiles/rN_c3_sq_counters.json from the SQ counter pass of scripts/gpu_final2.sh.
 
-usage: python scripts/sq_summary.py gpurun_out/TAG OUT.json ["kernel name substring"]
+usage: python scripts/sq_summary.py gpurun_out/TAG OUT.json ["kernel name substring"] [config]
 Per dispatch of the kernel: duration from the pass's own timestamps, clock =
 GRBM_GUI_ACTIVE / 8 XCDs / duration, MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES /
 1024 SIMDs / per-XCD GRBM cycles, SQ_* as fractions of SQ_WAVE_CYCLES."""
@@ -11,6 +11,7 @@ import sys
 
 root, out = sys.argv[1], sys.argv[2]
 kname = sys.argv[3] if len(sys.argv) > 3 else "k_fused<4, 8, true, 0, false>"
+cfg = sys.argv[4] if len(sys.argv) > 4 else "c3"
 per = collections.defaultdict(lambda: {"raw": collections.defaultdict(float)})
 for r in csv.DictReader(open(f"{root}/pmc_sq/run_counter_collection.csv")):
     if kname not in r["Kernel_Name"]:
@@ -23,22 +24,31 @@ for disp in sorted(per):
     d = per[disp]
     raw = d["raw"]
     grbm = raw["GRBM_GUI_ACTIVE"] / 8.0
-    wc = raw["SQ_WAVE_CYCLES"]
-    rows.append({"dispatch": disp, "duration_ms": d["duration_ms"],
-                 "clock_ghz": grbm / (d["duration_ms"] * 1e6),
-                 "mfma_busy_per_simd": raw["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024.0 / grbm,
-                 "active_inst_any": raw["SQ_ACTIVE_INST_ANY"] / wc, "active_inst_valu": raw["SQ_ACTIVE_INST_VALU"] / wc,
-                 "wait_inst_any": raw["SQ_WAIT_INST_ANY"] / wc, "wait_any": raw["SQ_WAIT_ANY"] / wc,
-                 "raw": dict(raw)})
+    wc = raw.get("SQ_WAVE_CYCLES", 0.0) or 1.0
+    row = {"dispatch": disp, "duration_ms": d["duration_ms"], "clock_ghz": grbm / (d["duration_ms"] * 1e6)}
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in raw:
+        row["mfma_busy_per_simd"] = raw["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024.0 / grbm
+    # SQ_* cycle counters as fractions of SQ_WAVE_CYCLES (quad-cycle units
+    # cancel); LDS-array cycles per CU cycle (256 CUs)
+    for name in ("SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_LDS",
+                 "SQ_ACTIVE_INST_LDS", "SQ_BUSY_CYCLES"):
+        if name in raw:
+            row[name.lower()[3:]] = raw[name] / wc
+    if "SQ_LDS_IDX_ACTIVE" in raw:
+        row["lds_active_per_cu_cycle"] = raw["SQ_LDS_IDX_ACTIVE"] / 256.0 / grbm
+    if "SQ_LDS_BANK_CONFLICT" in raw and "SQ_LDS_IDX_ACTIVE" in raw:
+        row["lds_conflict_frac"] = raw["SQ_LDS_BANK_CONFLICT"] / max(raw["SQ_LDS_IDX_ACTIVE"], 1.0)
+    row["raw"] = dict(raw)
+    rows.append(row)
 # gated no-op dispatches (a stopped batch's later launches) are left out, as
 # in scripts/trace_summary.py: shorter than 1% of the longest dispatch
 longest = max(r["duration_ms"] for r in rows)
 rows = [r for r in rows if r["duration_ms"] >= 0.01 * longest]
 mean = {k: sum(r[k] for r in rows) / len(rows) for k in rows[0] if k not in ("dispatch", "raw")}
-json.dump({"kernel": f"{kname} (c3)",
-           "source": "rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY "
-                     "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES -- python3 bench.py "
-                     "--steps 3 --warmup 1 --no-cpu-baseline (scripts/gpu_final2.sh)",
+ctrs = sorted(rows[0]["raw"]) if rows else []
+json.dump({"kernel": f"{kname} ({cfg})",
+           "source": f"rocprofv3 --pmc {' '.join(ctrs)} -- python3 bench.py --config {cfg} --warmup 1 "
+                     "--no-cpu-baseline (scripts/gpu_sq.sh)",
            "notes": "clock = GRBM_GUI_ACTIVE/8 XCDs / dispatch duration; MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / "
                     "1024 SIMDs / per-XCD GRBM cycles; SQ_* fractions of SQ_WAVE_CYCLES (quad-cycle units cancel)",
            "mean": mean, "dispatches": rows}, open(out, "w"), indent=1)

@@ -104,7 +104,7 @@ def test_c3_class_selects_s1():
 @pytest.mark.parametrize("n,d,k,centers", [
     (60000, 64, 256, 256),   # c3 shape: dp 64, kp 256
     (30000, 20, 100, 50),    # dp 32, kp 128 (pads)
-    (30000, 32, 512, 300),   # dp 32, kp 512 (16 members per chain)
+    (30000, 32, 250, 300),   # dp 32, kp 256 (8 members per chain, 1 MFMA k-slice)
     (20000, 128, 128, 128),  # dp 128, kp 128
     (20000, 64, 70, 40),     # kp 128, 58 pad slots
 ])
@@ -221,7 +221,7 @@ def test_fit_noise_delta_iterations():
 
 @pytest.mark.parametrize("n,d,k,centers", [
     (30000, 20, 100, 50),
-    (30000, 32, 512, 300),
+    (30000, 32, 250, 300),
     (20000, 128, 128, 128),
     (20000, 64, 70, 40),
 ])
