@@ -68,8 +68,8 @@ constexpr int S1_WAVES = 8;                     // 512 threads: two waves per SI
 constexpr int S1_LMAX = 4;                      // candidates re-scored per row
 constexpr int S1_RING = 16;                     // rows per re-scoring batch (one per quad of a wave)
 
-// the re-scoring batches run where a wave's ring (S1_RING rows of DP floats
-// + 16 B) fits beside the tables: dp <= 64
+// the re-scoring batches run where a wave's ring (S1_RING rows of DP floats,
+// 16 B of row data and 128 B of chain heads) fits beside the tables: dp <= 64
 constexpr bool s1_batched(int ns2) { return ns2 <= 2; }
 
 constexpr int ceil_log2_c(int v) { return v <= 1 ? 0 : 1 + ceil_log2_c((v + 1) / 2); }
@@ -297,11 +297,12 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
   float* sCf = reinterpret_cast<float*>(smem + KP * DP * 2);  // [NT][CS]
   float* sCn = sCf + NT * CS;                                 // [KP] output order
   int32_t* sPerm = reinterpret_cast<int32_t*>(sCn + KP);      // [NT]
-  // per wave: the re-scoring ring, rows' x [S1_RING][DP] and {row, old | cnt
-  // << 16, s0 | s1 << 16, s2 | s3 << 16}
+  // per wave: the re-scoring ring, rows' x [S1_RING][DP], {row, old | cnt
+  // << 16, s0 | s1 << 16, second head} and the 32 chain heads [4 lanes][8]
   constexpr bool BATCH = s1_batched(NS2);
   float* sRx = reinterpret_cast<float*>(sPerm + NT);                   // [S1_WAVES][S1_RING][DP]
   uint4* sRm = reinterpret_cast<uint4*>(sRx + S1_WAVES * S1_RING * DP);  // [S1_WAVES][S1_RING]
+  float4* sRh = reinterpret_cast<float4*>(sRm + S1_WAVES * S1_RING);     // [S1_WAVES][S1_RING][4][2]
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -477,7 +478,22 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
 #pragma unroll
       for (int u = 0; u < FQ / 4; ++u) xv[u] = xs[u];
       const uint32_t cnt = mt.y >> 16;
-      const uint32_t sl[4] = {mt.z & 0xFFFFu, mt.z >> 16, mt.w & 0xFFFFu, mt.w >> 16};
+      uint32_t sl[4] = {mt.z & 0xFFFFu, mt.z >> 16, 0u, 0u};
+      if (__ballot(act && cnt >= 3u) != 0ull) {
+        // candidates 3 and 4: the row's smallest heads above the second
+        const float4* hp = sRh + ((wave * S1_RING + slot) * 4 + q) * 2;
+        const float4 h0 = hp[0], h1 = hp[1];
+        const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        float prev = u2f(mt.w);
+#pragma unroll
+        for (int r = 2; r < S1_LMAX; ++r) {
+          float nl = FLT_MAX;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) nl = __builtin_fminf(nl, hv[i] > prev ? hv[i] : FLT_MAX);
+          prev = quad_min(nl);
+          sl[r] = (uint32_t)r < cnt ? (f2u(prev) & SLOTM) : 0u;
+        }
+      }
       int32_t lab1 = 0, lab2 = 0;
       uint32_t kind = 2u;
       decide(act, cnt, sl, xv, lab1, lab2, kind);
@@ -567,40 +583,45 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
       // while this one updates its keys
       __builtin_amdgcn_sched_barrier(0);
     }
-    // full slot ids in the heads, (chain << MB) | member, as order-preserving
-    // integers: the candidate count and the rounds below compare distinct
-    // keys exactly, whatever the float mode does with tiny values
-    int32_t hk[2][4];
+    // full slot ids in the heads, (chain << MB) | member: distinct keys, so
+    // float comparisons order them totally (f32 denormals are kept, and +0
+    // and -0 could only share a slot); non-finite rows are caught by `bad`
+    float hk[2][4];
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) hk[cb][i] = mono(f2u(h[cb][i]) | qbits | ((uint32_t)(16 * cb + i) << MB));
+      for (int i = 0; i < 4; ++i) hk[cb][i] = u2f(f2u(h[cb][i]) | qbits | ((uint32_t)(16 * cb + i) << MB));
+    // the smallest second key of the lane's chains (an open chain: h2 <= T)
+    const float h2m = __builtin_fminf(
+        __builtin_fminf(__builtin_fminf(h2[0][0], h2[0][1]), __builtin_fminf(h2[0][2], h2[0][3])),
+        __builtin_fminf(__builtin_fminf(h2[1][0], h2[1][1]), __builtin_fminf(h2[1][2], h2[1][3])));
 
     // the row's two smallest heads (m and the second candidate), then the
     // candidate threshold T: the lane's lowest two (med3 keeps the middle of
     // a sorted pair and a new value), merged over the quad
-    int32_t la = INT32_MAX, lb = INT32_MAX;
+    auto mn = [](float a, float b) { return __builtin_fminf(a, b); };
+    auto mx = [](float a, float b) { return __builtin_fmaxf(a, b); };
+    float la = FLT_MAX, lb = FLT_MAX;
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        lb = max(la, min(lb, hk[cb][i]));  // med3 (la <= lb)
-        la = min(la, hk[cb][i]);
+        lb = __builtin_amdgcn_fmed3f(la, lb, hk[cb][i]);  // (la <= lb)
+        la = mn(la, hk[cb][i]);
       }
     {
-      auto p = __builtin_amdgcn_permlane16_swap((uint32_t)la, (uint32_t)la, false, false);
-      auto p2 = __builtin_amdgcn_permlane16_swap((uint32_t)lb, (uint32_t)lb, false, false);
-      int32_t a0 = (int32_t)p[0], a1 = (int32_t)p[1], b0 = (int32_t)p2[0], b1 = (int32_t)p2[1];
-      la = min(a0, a1);
-      lb = min(max(a0, a1), min(b0, b1));
-      p = __builtin_amdgcn_permlane32_swap((uint32_t)la, (uint32_t)la, false, false);
-      p2 = __builtin_amdgcn_permlane32_swap((uint32_t)lb, (uint32_t)lb, false, false);
-      a0 = (int32_t)p[0], a1 = (int32_t)p[1], b0 = (int32_t)p2[0], b1 = (int32_t)p2[1];
-      la = min(a0, a1);
-      lb = min(max(a0, a1), min(b0, b1));
+      auto p = __builtin_amdgcn_permlane16_swap(f2u(la), f2u(la), false, false);
+      auto p2 = __builtin_amdgcn_permlane16_swap(f2u(lb), f2u(lb), false, false);
+      float a0 = u2f(p[0]), a1 = u2f(p[1]), b0 = u2f(p2[0]), b1 = u2f(p2[1]);
+      la = mn(a0, a1);
+      lb = mn(mx(a0, a1), mn(b0, b1));
+      p = __builtin_amdgcn_permlane32_swap(f2u(la), f2u(la), false, false);
+      p2 = __builtin_amdgcn_permlane32_swap(f2u(lb), f2u(lb), false, false);
+      a0 = u2f(p[0]), a1 = u2f(p[1]), b0 = u2f(p2[0]), b1 = u2f(p2[1]);
+      la = mn(a0, a1);
+      lb = mn(mx(a0, a1), mn(b0, b1));
     }
-    const int32_t mki = la;
-    const float m = u2f(unmono(mki));
+    const float m = la;
     const float xn = B.xn;
     const float E = fmaf(e1, xn, e0);
     const bool bad = !(m >= -3.0e38f && m <= 3.0e38f) || !(xn <= 3.0e38f);
@@ -612,20 +633,18 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     constexpr float IM = (1.0f / (1.0f + RP)) * (1.0f - 2.0f * U24);
     float T = R * (R >= 0.0f ? IP : IM);
     T = T * (T >= 0.0f ? (1.0f + 4.0f * U24) : (1.0f - 4.0f * U24));
-    const int32_t Tk = mono(f2u(T));
-    // candidates: heads <= T (low 16 bits of the quad sum); chains whose
+    // candidates: heads <= T (low 16 bits of the quad sum); a chain whose
     // second key is <= T too (high 16 bits: the row goes to the full scan)
-    uint32_t cl = 0;
+    uint32_t cl = (h2m <= T) ? 0x10000u : 0u;
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        cl += ((hk[cb][i] <= Tk) ? 1u : 0u) + ((h2[cb][i] <= T) ? 0x10000u : 0u);
+      for (int i = 0; i < 4; ++i) cl += (hk[cb][i] <= T) ? 1u : 0u;
     const uint32_t cq = bad ? 0u : quad_add_u(cl);
     const uint32_t cnt = cq & 0xFFFFu;
     const bool ovf = (cq >> 16) != 0u;
 
-    const uint32_t sm = unmono(mki) & SLOTM;
+    const uint32_t sm = f2u(la) & SLOTM;
     const bool ok = valid && !bad && !ovf;
     const bool needy = ok && cnt >= 2u && cnt <= (uint32_t)S1_LMAX;
     const int32_t labm = sPerm[sm];
@@ -636,36 +655,27 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     if constexpr (MODE == 1) old = (int32_t)min((uint32_t)B.old, (uint32_t)(A.k - 1));
     if constexpr (BATCH) {
       emit(valid && !needy, row, dec1 ? 0u : 2u, labm, 0, old);
-      // rows with 2..LMAX candidates: into the wave's ring with their
-      // candidates in ascending key order (the first two are the row's two
-      // smallest heads); a full ring is re-scored as one batch
+      // rows with 2..LMAX candidates: into the wave's ring with their two
+      // smallest heads' slots (and, for 3 or more candidates, every chain
+      // head, from which the batch extracts the rest); a full ring is
+      // re-scored as one batch
       const uint64_t mrow = __ballot(needy && q == 0);
       if (mrow) {
-        uint32_t s2c = 0, s3c = 0;
-        if (__ballot(needy && cnt >= 3u) != 0ull) {
-          int32_t prev = lb;
-#pragma unroll
-          for (int r = 2; r < S1_LMAX; ++r) {
-            int32_t nl = INT32_MAX;
-#pragma unroll
-            for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-              for (int i = 0; i < 4; ++i) nl = min(nl, hk[cb][i] > prev ? hk[cb][i] : INT32_MAX);
-            prev = quad_min_i(nl);
-            const uint32_t sl = (uint32_t)r < cnt ? (unmono(prev) & SLOTM) : 0u;
-            if (r == 2) s2c = sl; else s3c = sl;
-          }
-        }
         const uint32_t nn = (uint32_t)__popcll(mrow);
         const uint32_t rk = (uint32_t)__popcll(mrow & ((1ull << c16) - 1ull));
         const uint32_t space = (uint32_t)S1_RING - rc;
-        const uint4 meta = make_uint4(row, (uint32_t)old | (cnt << 16), sm | ((unmono(lb) & SLOTM) << 16),
-                                      s2c | (s3c << 16));
+        const uint4 meta = make_uint4(row, (uint32_t)old | (cnt << 16), sm | ((f2u(lb) & SLOTM) << 16), f2u(lb));
         auto stash = [&](uint32_t slot) {
           float4* xs = reinterpret_cast<float4*>(sRx + (wave * S1_RING + slot) * DP + FQ * q);
 #pragma unroll
           for (int u = 0; u < FQ / 4; ++u) xs[u] = B.x[u];
           if (q == 0) sRm[wave * S1_RING + slot] = meta;
+          // the heads only matter with 3 or more candidates
+          if (cnt >= 3u) {
+            float4* hp = sRh + ((wave * S1_RING + slot) * 4 + q) * 2;
+            hp[0] = make_float4(hk[0][0], hk[0][1], hk[0][2], hk[0][3]);
+            hp[1] = make_float4(hk[1][0], hk[1][1], hk[1][2], hk[1][3]);
+          }
         };
         if (needy && rk < space) stash(rc + rk);
         if (nn >= space) {
@@ -680,19 +690,19 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
       // dp > 64: the candidates re-scored in the tile, every row of it
       uint32_t sl[S1_LMAX];
       sl[0] = sm;
-      sl[1] = unmono(lb) & SLOTM;
-      int32_t prev = lb;
+      sl[1] = f2u(lb) & SLOTM;
+      float prev = lb;
 #pragma unroll
       for (int r = 2; r < S1_LMAX; ++r) {
         sl[r] = 0u;
         if (__ballot(needy && (uint32_t)r < cnt) == 0ull) continue;
-        int32_t nl = INT32_MAX;
+        float nl = FLT_MAX;
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) nl = min(nl, hk[cb][i] > prev ? hk[cb][i] : INT32_MAX);
-        prev = quad_min_i(nl);
-        sl[r] = unmono(prev) & SLOTM;
+          for (int i = 0; i < 4; ++i) nl = __builtin_fminf(nl, hk[cb][i] > prev ? hk[cb][i] : FLT_MAX);
+        prev = quad_min(nl);
+        sl[r] = f2u(prev) & SLOTM;
       }
       int32_t lab1 = labm, lab2 = 0;
       uint32_t kind = dec1 ? 0u : 2u;
@@ -928,7 +938,7 @@ hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, cons
   ql->nwaves = (uint32_t)nw;
   S1Args a{X, xnorm, g.n, g.k, g.d, seg, img, cn2o, cft, perm, cst, labels, queue, qcount, chg, chg_cnt, gate};
   const size_t lds = (size_t)g.kp * g.dp * 2 + (size_t)nt * (g.dp + 4) * 4 + (size_t)g.kp * 4 + (size_t)nt * 4 +
-                     (s1_batched(sg.ns2) ? (size_t)S1_WAVES * S1_RING * (g.dp * 4 + 16) : 0);
+                     (s1_batched(sg.ns2) ? (size_t)S1_WAVES * S1_RING * (g.dp * 4 + 16 + 128) : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
 #define KM_S1_CASE(NS2_, NB_)                                                                                   \
   case NS2_ * 100 + NB_:                                                                                        \
