@@ -66,6 +66,15 @@ constexpr float U24 = 5.9604644775390625e-08f;  // 2^-24
 constexpr float U16 = 4.8828125e-04f;           // 2^-11, fp16 unit roundoff
 constexpr int S1_WAVES = 8;                     // 512 threads: two waves per SIMD
 constexpr int S1_LMAX = 4;                      // candidates re-scored per row
+#ifndef KM_S1_PIPE
+#define KM_S1_PIPE 0  // A/B knob: round 5, no gain
+#endif
+#ifndef KM_S1_NBUF
+#define KM_S1_NBUF 2  // register buffers of rows (tiles in flight + 1)
+#endif
+#ifndef KM_S1_ABL
+#define KM_S1_ABL 0   // timing ablations (wrong labels): never in the product library
+#endif
 constexpr int S1_RING = 16;                     // rows per re-scoring batch (one per quad of a wave)
 
 // the re-scoring batches run where a wave's ring (S1_RING rows of DP floats,
@@ -130,8 +139,10 @@ struct S1Geo {
 // workgroup).  In index order, centroid j joins the non-full chain whose
 // members are farthest from it (largest minimum distance; ties: lowest
 // chain).  perm[(chain << mb) | member] = centroid, -1 for pads.  Only a
-// cost choice: the certificate uses R_c computed for whatever colouring is
-// current, so a stale or poor colouring can queue rows, never mislabel them.
+// cost choice: the certificate (a chain whose second key is under the
+// threshold sends its row to the full scan) holds for any colouring, so a
+// stale or poor one (it is recomputed once per batch) can queue rows, never
+// mislabel them.
 // ---------------------------------------------------------------------------
 template <int DPC>
 __global__ __launch_bounds__(512) void k_s1_color(const float* __restrict__ C32, int k, int dp, int nb, int mb,
@@ -550,39 +561,63 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     load_pair(0, pr[0]);
     // blocks in pairs: two members per step, new best = min3(best, ka, kb),
     // new second = min(second, med3(best, ka, kb))
+    auto mfma_pair = [&](const Pair& P, f32x4 (&a)[2][2]) {
 #pragma unroll
-    for (int blk = 0; blk < NB; blk += 2) {
-      const Pair& P = pr[(blk >> 1) & 1];
-      if (blk + 2 < NB) load_pair(blk + 2, pr[((blk >> 1) + 1) & 1]);
-      f32x4 a0[2], a1[2];
+      for (int e = 0; e < 2; ++e)
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        a0[cb] = f32x4{P.c[0][cb].x, P.c[0][cb].y, P.c[0][cb].z, P.c[0][cb].w};
-        a1[cb] = f32x4{P.c[1][cb].x, P.c[1][cb].y, P.c[1][cb].z, P.c[1][cb].w};
-      }
+        for (int cb = 0; cb < 2; ++cb) a[e][cb] = f32x4{P.c[e][cb].x, P.c[e][cb].y, P.c[e][cb].z, P.c[e][cb].w};
 #pragma unroll
       for (int t = 0; t < NS2; ++t)
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          a0[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(P.a[0][cb][t], bx[t], a0[cb], 0, 0, 0);
-          a1[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(P.a[1][cb][t], bx[t], a1[cb], 0, 0, 0);
-        }
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            a[e][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(P.a[e][cb][t], bx[t], a[e][cb], 0, 0, 0);
+    };
+    auto keys_pair = [&](int blk, const f32x4 (&a)[2][2]) {
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float ka = u2f((f2u(a0[cb][i]) & KMASK) | (uint32_t)blk);
-          const float kb = u2f((f2u(a1[cb][i]) & KMASK) | (uint32_t)(blk + 1));
+          const float ka = u2f((f2u(a[0][cb][i]) & KMASK) | (uint32_t)blk);
+          const float kb = u2f((f2u(a[1][cb][i]) & KMASK) | (uint32_t)(blk + 1));
           const float t = __builtin_amdgcn_fmed3f(h[cb][i], ka, kb);
           h[cb][i] = __builtin_fminf(__builtin_fminf(h[cb][i], ka), kb);
           h2[cb][i] = __builtin_fminf(h2[cb][i], t);
         }
+    };
+#if KM_S1_PIPE
+    // software-pipelined: pair p's MFMAs are issued with pair p - 1's key
+    // updates in one scheduling region (independent: the VALU work fills the
+    // MFMA issue gaps of this wave), the next pair's operands read meanwhile
+    f32x4 acc[2][2][2];
+    if (2 < NB) load_pair(2, pr[1]);
+    mfma_pair(pr[0], acc[0]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int blk = 2; blk < NB; blk += 2) {
+      const int cur = (blk >> 1) & 1;
+      mfma_pair(pr[cur], acc[cur]);
+      if (blk + 2 < NB) load_pair(blk + 2, pr[cur ^ 1]);
+      keys_pair(blk - 2, acc[cur ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    keys_pair(NB - 2, acc[((NB - 2) >> 1) & 1]);
+#else
+#pragma unroll
+    for (int blk = 0; blk < NB; blk += 2) {
+      const Pair& P = pr[(blk >> 1) & 1];
+      if (blk + 2 < NB) load_pair(blk + 2, pr[((blk >> 1) + 1) & 1]);
+      f32x4 a[2][2];
+      mfma_pair(P, a);
+      keys_pair(blk, a);
       // one block pair in flight (plus the next one's operands): the
       // scheduler would otherwise hoist every pair's reads and MFMAs ahead of
       // the key updates; the partner wave on the SIMD fills the MFMA pipe
       // while this one updates its keys
       __builtin_amdgcn_sched_barrier(0);
     }
+#endif
     // full slot ids in the heads, (chain << MB) | member: distinct keys, so
     // float comparisons order them totally (f32 denormals are kept, and +0
     // and -0 could only share a slot); non-finite rows are caught by `bad`
@@ -622,6 +657,11 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
       lb = mn(mx(a0, a1), mn(b0, b1));
     }
     const float m = la;
+#if KM_S1_ABL == 1
+    // ablation (timing only, wrong labels): the screen core alone
+    if (valid && q == 0) A.labels[row] = sPerm[f2u(la) & SLOTM] + (h2[0][0] < -1e30f ? 1 : 0);
+    return;
+#endif
     const float xn = B.xn;
     const float E = fmaf(e1, xn, e0);
     const bool bad = !(m >= -3.0e38f && m <= 3.0e38f) || !(xn <= 3.0e38f);
@@ -653,6 +693,11 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     const bool dec1 = ok && cnt == 1u && labm >= 0;
     int32_t old = 0;
     if constexpr (MODE == 1) old = (int32_t)min((uint32_t)B.old, (uint32_t)(A.k - 1));
+#if KM_S1_ABL == 2
+    // ablation (timing only, wrong labels): no re-scoring
+    emit(valid, row, dec1 || needy ? 0u : 2u, labm, 0, old);
+    return;
+#endif
     if constexpr (BATCH) {
       emit(valid && !needy, row, dec1 ? 0u : 2u, labm, 0, old);
       // rows with 2..LMAX candidates: into the wave's ring with their two
@@ -714,6 +759,23 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
   // this wave's tiles gw, gw + nw, ...: two register buffers, the next
   // tile's loads in flight while one is processed (loads past the end read
   // row n - 1 and are never used)
+#if KM_S1_NBUF == 3
+  // three register buffers: two tiles' loads in flight while one is
+  // processed (tile + 4 nw stays below 2^32: ntiles < 2^28, nw < 2^16)
+  Buf b0, b1, b2;
+  load(gw, b0);
+  load(gw + nw, b1);
+  for (uint32_t tile = gw; tile < ntiles; tile += 3 * nw) {
+    load(tile + 2 * nw, b2);
+    process(tile, b0);
+    if (tile + nw >= ntiles) break;
+    load(tile + 3 * nw, b0);
+    process(tile + nw, b1);
+    if (tile + 2 * nw >= ntiles) break;
+    load(tile + 4 * nw, b1);
+    process(tile + 2 * nw, b2);
+  }
+#else
   Buf b0, b1;
   load(gw, b0);
   // (tile + 2 nw stays below 2^32: ntiles < 2^28, nw < 2^16)
@@ -724,6 +786,7 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     load(tile + 2 * nw, b0);
     process(tile + nw, b1);
   }
+#endif
   if (rc) rescore(rc);
   if (lane == 0) {
     A.qcount[2 * gw] = qn;
