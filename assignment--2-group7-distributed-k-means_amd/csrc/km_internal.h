@@ -240,6 +240,8 @@ hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, cons
 // k_s1's change list: entries (wave segments) and per-wave counts to allocate
 size_t s1_chg_entries(const Geometry& g, int n_cu);
 size_t s1_wave_slots(int n_cu);
+// delta statistics possible (k_s1_delta's table fits LDS)
+bool s1_delta_ok(const Geometry& g, int n_cu);
 // delta statistics: the change list of k_s1 into stats (deltas)
 hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt,
                            double* stats, int n_cu, const int* gate, hipStream_t s);

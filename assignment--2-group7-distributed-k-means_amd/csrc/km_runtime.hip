@@ -434,11 +434,11 @@ int run_assign(km_ctx* c, bool with_stats);
 
 // k_s1 for this assign: labels only (predict), or delta statistics once the
 // labels and the full sums of a previous iteration are in place (no SSE: its
-// residuals need every row, KM_SCREEN_S1 keeps the full-statistics screen)
+// residuals need every row; and only where k_s1_delta's table fits LDS)
 bool use_s1(km_ctx* c, bool with_stats) {
   if (!c->s1) return false;
   if (c->screen_forced >= 0 && c->screen_forced != KM_SCREEN_S1) return false;
-  return !with_stats || (c->delta_ready && !c->want_sse);
+  return !with_stats || (c->delta_ready && !c->want_sse && km::s1_delta_ok(c->g, c->n_cu));
 }
 
 // before an update reads the statistics: delta -> fold into the full sums;
@@ -482,7 +482,7 @@ int run_assign(km_ctx* c, bool with_stats) {
     return KM_OK;
   }
   c->stats_pending = with_stats ? 1 : 0;
-  if (c->fused && use_s1(c, with_stats)) {
+  if (use_s1(c, with_stats)) {
     {
       ProfScope ps(c, KM_K_ASSIGN, true);
       KM_HIP(km::launch_s1(c->X, c->xnorm, g, c->s1_img, c->s1_cn2o, c->s1_cft, c->s1_perm, c->s1_cst,
@@ -525,6 +525,20 @@ int run_assign(km_ctx* c, bool with_stats) {
     }
     return KM_OK;  // counts are part of the fused and resolver statistics
   }
+  if (c->s1 && !c->fused && (c->screen_forced < 0 || c->screen_forced == KM_SCREEN_S1)) {
+    // unfused geometry (c4 class): k_s1's labels (queued rows resolved in
+    // float64), then the statistics pass below reads X once more
+    {
+      ProfScope ps(c, KM_K_ASSIGN, true);
+      KM_HIP(km::launch_s1(c->X, c->xnorm, g, c->s1_img, c->s1_cn2o, c->s1_cft, c->s1_perm, c->s1_cst, c->labels,
+                           c->queue, c->qcount, c->chg, c->chg_cnt, 0, c->n_cu, &c->ql, c->gate, c->stream));
+    }
+    {
+      ProfScope ps(c, KM_K_RESOLVE);
+      KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels, nullptr,
+                                c->n_cu, c->gate, c->stream));
+    }
+  } else {
   if (!c->cand && g.dp <= 256) {
     // candidate lists of the points the screen cannot settle between its top
     // two (kind 4): up to 4M records of 64 B; a full pool leaves the rest to
@@ -544,6 +558,7 @@ int run_assign(km_ctx* c, bool with_stats) {
     ProfScope ps(c, KM_K_RESOLVE);
     KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels, nullptr, c->n_cu,
                               c->gate, c->stream, nullptr, c->cand, c->cand_cap));
+  }
   }
   if (with_stats) {
     ProfScope ps(c, KM_K_STATS);
@@ -795,7 +810,9 @@ int km_set_screen(km_ctx* c, int32_t mode) {
 int km_get_screen(km_ctx* c, int32_t* mode) {
   KM_REQUIRE(c && mode, KM_ERR_ARG, "null ctx");
   // the screen of the next fused assign with statistics
-  *mode = (c->fused && use_s1(c, true)) ? KM_SCREEN_S1 : c->screen;
+  *mode = (use_s1(c, true) || (c->s1 && !c->fused && (c->screen_forced < 0 || c->screen_forced == KM_SCREEN_S1)))
+              ? KM_SCREEN_S1
+              : c->screen;
   return KM_OK;
 }
 
@@ -864,7 +881,10 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
     else
       c->path = 0;
     c->fused = (c->path == 2) && km::fused_path_ok(c->g) && !fused_disabled();
-    c->s1 = c->fused && km::fused16_ok(c->g) && km::s1_ok(c->g) && km::diag_env("KM_S1", 1) != 0;
+    // k_s1 beside the fused screen (c3 class: delta statistics) or in place
+    // of the unfused screen (c4 class: labels, then the statistics pass)
+    c->s1 = (c->path == 2) && (!c->fused || km::fused16_ok(c->g)) && km::s1_ok(c->g) &&
+            km::diag_env("KM_S1", 1) != 0;
     if (c->s1) {
       const size_t nt = km::s1_table_entries(c->g);
       KM_HIP(hipMalloc(&c->s1_perm, sizeof(int32_t) * nt));

@@ -65,23 +65,30 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr float U24 = 5.9604644775390625e-08f;  // 2^-24
 constexpr float U16 = 4.8828125e-04f;           // 2^-11, fp16 unit roundoff
 constexpr int S1_WAVES = 8;                     // 512 threads: two waves per SIMD
-constexpr int S1_LMAX = 4;                      // candidates re-scored per row
-#ifndef KM_S1_PIPE
-#define KM_S1_PIPE 0  // A/B knob: round 5, no gain
-#endif
+constexpr int S1_LMAX = 8;                      // candidates re-scored per row
 #ifndef KM_S1_NBUF
-#define KM_S1_NBUF 2  // register buffers of rows (tiles in flight + 1)
+#define KM_S1_NBUF 0  // register buffers of rows (tiles in flight + 1); 0: by row length
 #endif
 #ifndef KM_S1_ABL
 #define KM_S1_ABL 0   // timing ablations (wrong labels): never in the product library
 #endif
+constexpr int ceil_log2_c(int v) { return v <= 1 ? 0 : 1 + ceil_log2_c((v + 1) / 2); }
 constexpr int S1_RING = 16;                     // rows per re-scoring batch (one per quad of a wave)
 
 // the re-scoring batches run where a wave's ring (S1_RING rows of DP floats,
 // 16 B of row data and 128 B of chain heads) fits beside the tables: dp <= 64
 constexpr bool s1_batched(int ns2) { return ns2 <= 2; }
 
-constexpr int ceil_log2_c(int v) { return v <= 1 ? 0 : 1 + ceil_log2_c((v + 1) / 2); }
+// k_s1's LDS: image, fp32 table (unless it goes to global), norms, slots,
+// re-scoring rings; the table goes to global memory where all of it would
+// not fit one workgroup's 160 KiB
+constexpr size_t s1_lds_bytes(int ns2, int nb, bool table) {
+  const int dp = 32 * ns2, kp = 32 * nb, nt = 32 << ceil_log2_c(nb);
+  return (size_t)kp * dp * 2 + (table ? (size_t)nt * (dp + 4) * 4 : 0) + (size_t)kp * 4 + (size_t)nt * 4 +
+         (s1_batched(ns2) ? (size_t)S1_WAVES * S1_RING * (dp * 4 + 16 + 128) : 0);
+}
+constexpr bool s1_table_global(int ns2, int nb) { return s1_lds_bytes(ns2, nb, true) > 160 * 1024; }
+
 
 __device__ __forceinline__ uint32_t f2u(float v) { return __float_as_uint(v); }
 __device__ __forceinline__ float u2f(uint32_t v) { return __uint_as_float(v); }
@@ -144,13 +151,13 @@ struct S1Geo {
 // stale or poor one (it is recomputed once per batch) can queue rows, never
 // mislabel them.
 // ---------------------------------------------------------------------------
-template <int DPC>
-__global__ __launch_bounds__(512) void k_s1_color(const float* __restrict__ C32, int k, int dp, int nb, int mb,
+template <int DPC, int NTH>
+__global__ __launch_bounds__(NTH) void k_s1_color(const float* __restrict__ C32, int k, int dp, int nb, int mb,
                                                   int32_t* __restrict__ perm, const int* __restrict__ gate) {
   if (*gate) return;
   __shared__ unsigned int cmin[32];
   __shared__ int cnt[32];
-  __shared__ int cls[512];
+  __shared__ int cls[NTH];
   const int t = threadIdx.x;
   float cv[DPC];
 #pragma unroll
@@ -303,14 +310,17 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
   constexpr uint32_t KMASK = ~SLOTM;
   // key packing perturbation: the low 5 + MB mantissa bits replaced
   constexpr float RHO = (float)SLOTM * 1.1920928955078125e-07f * 1.0001f;
+  // the fp32 table stays in global memory (L2) where it does not fit LDS
+  // beside the image (s1_lds_bytes)
+  constexpr bool BATCH = s1_batched(NS2);
+  constexpr bool TG = s1_table_global(NS2, NB);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint4* sImg = reinterpret_cast<const uint4*>(smem);    // [NB][2][NS2][64] A fragments
-  float* sCf = reinterpret_cast<float*>(smem + KP * DP * 2);  // [NT][CS]
-  float* sCn = sCf + NT * CS;                                 // [KP] output order
+  float* sCf = reinterpret_cast<float*>(smem + KP * DP * 2);  // [NT][CS] (not with TG)
+  float* sCn = sCf + (TG ? 0 : NT * CS);                      // [KP] output order
   int32_t* sPerm = reinterpret_cast<int32_t*>(sCn + KP);      // [NT]
   // per wave: the re-scoring ring, rows' x [S1_RING][DP], {row, old | cnt
   // << 16, s0 | s1 << 16, second head} and the 32 chain heads [4 lanes][8]
-  constexpr bool BATCH = s1_batched(NS2);
   float* sRx = reinterpret_cast<float*>(sPerm + NT);                   // [S1_WAVES][S1_RING][DP]
   uint4* sRm = reinterpret_cast<uint4*>(sRx + S1_WAVES * S1_RING * DP);  // [S1_WAVES][S1_RING]
   float4* sRh = reinterpret_cast<float4*>(sRm + S1_WAVES * S1_RING);     // [S1_WAVES][S1_RING][4][2]
@@ -322,9 +332,11 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
   {
     uint4* di = reinterpret_cast<uint4*>(smem);
     for (int i = threadIdx.x; i < KP * DP / 8; i += S1_WAVES * 64) di[i] = A.img[i];
-    const float4* src = reinterpret_cast<const float4*>(A.cft);
-    float4* dst = reinterpret_cast<float4*>(sCf);
-    for (int i = threadIdx.x; i < NT * CS / 4; i += S1_WAVES * 64) dst[i] = src[i];
+    if constexpr (!TG) {
+      const float4* src = reinterpret_cast<const float4*>(A.cft);
+      float4* dst = reinterpret_cast<float4*>(sCf);
+      for (int i = threadIdx.x; i < NT * CS / 4; i += S1_WAVES * 64) dst[i] = src[i];
+    }
     for (int i = threadIdx.x; i < KP; i += S1_WAVES * 64) sCn[i] = A.cn2o[i];
     for (int i = threadIdx.x; i < NT; i += S1_WAVES * 64) sPerm[i] = A.perm[i];
   }
@@ -371,7 +383,8 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
   auto decide = [&](bool act0, uint32_t cnt, const uint32_t* sl, const float4* xv, int32_t& lab1, int32_t& lab2,
                     uint32_t& kind) {
     auto partial = [&](uint32_t slot) {
-      const float4* cp = reinterpret_cast<const float4*>(sCf + slot * CS + FQ * q);
+      const float4* cp = TG ? reinterpret_cast<const float4*>(A.cft + slot * CS + FQ * q)
+                            : reinterpret_cast<const float4*>(sCf + slot * CS + FQ * q);
       float acc = 0.0f;
 #pragma unroll
       for (int u = 0; u < FQ / 4; ++u) {
@@ -489,15 +502,20 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
 #pragma unroll
       for (int u = 0; u < FQ / 4; ++u) xv[u] = xs[u];
       const uint32_t cnt = mt.y >> 16;
-      uint32_t sl[4] = {mt.z & 0xFFFFu, mt.z >> 16, 0u, 0u};
+      uint32_t sl[S1_LMAX];
+      sl[0] = mt.z & 0xFFFFu;
+      sl[1] = mt.z >> 16;
+#pragma unroll
+      for (int r = 2; r < S1_LMAX; ++r) sl[r] = 0u;
       if (__ballot(act && cnt >= 3u) != 0ull) {
-        // candidates 3 and 4: the row's smallest heads above the second
+        // candidates 3, 4, ...: the row's smallest heads above the second
         const float4* hp = sRh + ((wave * S1_RING + slot) * 4 + q) * 2;
         const float4 h0 = hp[0], h1 = hp[1];
         const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
         float prev = u2f(mt.w);
 #pragma unroll
         for (int r = 2; r < S1_LMAX; ++r) {
+          if (__ballot(act && (uint32_t)r < cnt) == 0ull) break;
           float nl = FLT_MAX;
 #pragma unroll
           for (int i = 0; i < 8; ++i) nl = __builtin_fminf(nl, hv[i] > prev ? hv[i] : FLT_MAX);
@@ -586,38 +604,42 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
           h2[cb][i] = __builtin_fminf(h2[cb][i], t);
         }
     };
-#if KM_S1_PIPE
-    // software-pipelined: pair p's MFMAs are issued with pair p - 1's key
-    // updates in one scheduling region (independent: the VALU work fills the
-    // MFMA issue gaps of this wave), the next pair's operands read meanwhile
-    f32x4 acc[2][2][2];
-    if (2 < NB) load_pair(2, pr[1]);
-    mfma_pair(pr[0], acc[0]);
-    __builtin_amdgcn_sched_barrier(0);
+    // one block pair in flight (plus the next one's operands): the scheduler
+    // would otherwise hoist every pair's reads and MFMAs ahead of the key
+    // updates; the partner wave on the SIMD fills the MFMA pipe while this one
+    // updates its keys
+    if constexpr (NB <= 8) {
 #pragma unroll
-    for (int blk = 2; blk < NB; blk += 2) {
-      const int cur = (blk >> 1) & 1;
-      mfma_pair(pr[cur], acc[cur]);
-      if (blk + 2 < NB) load_pair(blk + 2, pr[cur ^ 1]);
-      keys_pair(blk - 2, acc[cur ^ 1]);
-      __builtin_amdgcn_sched_barrier(0);
+      for (int blk = 0; blk < NB; blk += 2) {
+        const Pair& P = pr[(blk >> 1) & 1];
+        if (blk + 2 < NB) load_pair(blk + 2, pr[((blk >> 1) + 1) & 1]);
+        f32x4 a[2][2];
+        mfma_pair(P, a);
+        keys_pair(blk, a);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+      // many members (NB a multiple of 4): two pairs per trip of a loop, the
+      // member id a run-time value
+      static_assert(NB % 4 == 0, "NB > 8 must be a multiple of 4");
+#pragma unroll 1
+      for (int blk = 0; blk < NB; blk += 4) {
+        load_pair(blk + 2, pr[1]);
+        {
+          f32x4 a[2][2];
+          mfma_pair(pr[0], a);
+          keys_pair(blk, a);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (blk + 4 < NB) load_pair(blk + 4, pr[0]);
+        {
+          f32x4 a[2][2];
+          mfma_pair(pr[1], a);
+          keys_pair(blk + 2, a);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
-    keys_pair(NB - 2, acc[((NB - 2) >> 1) & 1]);
-#else
-#pragma unroll
-    for (int blk = 0; blk < NB; blk += 2) {
-      const Pair& P = pr[(blk >> 1) & 1];
-      if (blk + 2 < NB) load_pair(blk + 2, pr[((blk >> 1) + 1) & 1]);
-      f32x4 a[2][2];
-      mfma_pair(P, a);
-      keys_pair(blk, a);
-      // one block pair in flight (plus the next one's operands): the
-      // scheduler would otherwise hoist every pair's reads and MFMAs ahead of
-      // the key updates; the partner wave on the SIMD fills the MFMA pipe
-      // while this one updates its keys
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#endif
     // full slot ids in the heads, (chain << MB) | member: distinct keys, so
     // float comparisons order them totally (f32 denormals are kept, and +0
     // and -0 could only share a slot); non-finite rows are caught by `bad`
@@ -759,34 +781,25 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
   // this wave's tiles gw, gw + nw, ...: two register buffers, the next
   // tile's loads in flight while one is processed (loads past the end read
   // row n - 1 and are never used)
-#if KM_S1_NBUF == 3
-  // three register buffers: two tiles' loads in flight while one is
-  // processed (tile + 4 nw stays below 2^32: ntiles < 2^28, nw < 2^16)
-  Buf b0, b1, b2;
-  load(gw, b0);
-  load(gw + nw, b1);
-  for (uint32_t tile = gw; tile < ntiles; tile += 3 * nw) {
-    load(tile + 2 * nw, b2);
-    process(tile, b0);
-    if (tile + nw >= ntiles) break;
-    load(tile + 3 * nw, b0);
-    process(tile + nw, b1);
-    if (tile + 2 * nw >= ntiles) break;
-    load(tile + 4 * nw, b1);
-    process(tile + 2 * nw, b2);
+  // NBUF register buffers of rows: NBUF - 1 tiles' loads in flight while
+  // one is processed (short rows need more of them to keep HBM busy)
+  constexpr int NBUF = KM_S1_NBUF > 0 ? KM_S1_NBUF : (NS2 == 1 ? 4 : 2);
+  Buf b[NBUF];
+#pragma unroll
+  for (int u = 0; u + 1 < NBUF; ++u) load(gw + (uint32_t)u * nw, b[u]);
+  // (tile + 2 NBUF nw stays below 2^32: ntiles < 2^28, nw < 2^16)
+  for (uint32_t tile = gw; tile < ntiles; tile += (uint32_t)NBUF * nw) {
+    bool done = false;
+#pragma unroll
+    for (int u = 0; u < NBUF; ++u) {
+      if (!done) {
+        load(tile + (uint32_t)(u + NBUF - 1) * nw, b[(u + NBUF - 1) % NBUF]);
+        process(tile + (uint32_t)u * nw, b[u]);
+        done = tile + (uint32_t)(u + 1) * nw >= ntiles;
+      }
+    }
+    if (done) break;
   }
-#else
-  Buf b0, b1;
-  load(gw, b0);
-  // (tile + 2 nw stays below 2^32: ntiles < 2^28, nw < 2^16)
-  for (uint32_t tile = gw; tile < ntiles; tile += 2 * nw) {
-    load(tile + nw, b1);
-    process(tile, b0);
-    if (tile + nw >= ntiles) break;
-    load(tile + 2 * nw, b0);
-    process(tile + nw, b1);
-  }
-#endif
   if (rc) rescore(rc);
   if (lane == 0) {
     A.qcount[2 * gw] = qn;
@@ -920,6 +933,14 @@ size_t s1_chg_entries(const Geometry& g, int n_cu) {
 
 size_t s1_wave_slots(int n_cu) { return (size_t)n_cu * S1_WAVES; }
 
+// the delta aggregation's LDS table [k][d+1] f64 and the wave-count prefix fit
+bool s1_delta_ok(const Geometry& g, int n_cu) {
+  int nbk;
+  uint32_t seg;
+  const int64_t nw = s1_grid(g, n_cu, &nbk, &seg);
+  return (size_t)g.k * (g.d + 1) * 8 + (size_t)(nw + 1) * 4 <= 160 * 1024 && g.k <= 65535;
+}
+
 hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt,
                            double* stats, int n_cu, const int* gate, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
@@ -945,7 +966,8 @@ bool s1_ok(const Geometry& g) {
   if (g.dp % 32 || g.kp % 64) return false;
   switch ((g.dp / 32) * 100 + g.kp / 32) {
     case 202: case 204: case 206: case 208:
-    case 102: case 104: case 106: case 108:
+    case 102: case 104: case 106: case 108: case 112: case 116: case 132:
+    case 216:
     case 402: case 404:
       return true;
     default:
@@ -965,11 +987,20 @@ size_t s1_table_entries(const Geometry& g) { return (size_t)32 << s1_geo(g).mb; 
 
 hipError_t launch_s1_color(const float* C32, const Geometry& g, int32_t* perm, const int* gate, hipStream_t s) {
   const S1Geo sg = s1_geo(g);
-  if (g.k > 512) return hipErrorInvalidValue;
+  if (g.k > (g.dp == 32 ? 1024 : 512)) return hipErrorInvalidValue;
   switch (g.dp) {
-    case 32: hipLaunchKernelGGL(k_s1_color<32>, dim3(1), dim3(512), 0, s, C32, g.k, g.dp, sg.nb, sg.mb, perm, gate); break;
-    case 64: hipLaunchKernelGGL(k_s1_color<64>, dim3(1), dim3(512), 0, s, C32, g.k, g.dp, sg.nb, sg.mb, perm, gate); break;
-    case 128: hipLaunchKernelGGL(k_s1_color<128>, dim3(1), dim3(512), 0, s, C32, g.k, g.dp, sg.nb, sg.mb, perm, gate); break;
+    case 32:
+      if (g.k > 512)
+        hipLaunchKernelGGL((k_s1_color<32, 1024>), dim3(1), dim3(1024), 0, s, C32, g.k, g.dp, sg.nb, sg.mb, perm, gate);
+      else
+        hipLaunchKernelGGL((k_s1_color<32, 512>), dim3(1), dim3(512), 0, s, C32, g.k, g.dp, sg.nb, sg.mb, perm, gate);
+      break;
+    case 64:
+      hipLaunchKernelGGL((k_s1_color<64, 512>), dim3(1), dim3(512), 0, s, C32, g.k, g.dp, sg.nb, sg.mb, perm, gate);
+      break;
+    case 128:
+      hipLaunchKernelGGL((k_s1_color<128, 512>), dim3(1), dim3(512), 0, s, C32, g.k, g.dp, sg.nb, sg.mb, perm, gate);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1000,9 +1031,9 @@ hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, cons
   ql->seg = seg;
   ql->nwaves = (uint32_t)nw;
   S1Args a{X, xnorm, g.n, g.k, g.d, seg, img, cn2o, cft, perm, cst, labels, queue, qcount, chg, chg_cnt, gate};
-  const size_t lds = (size_t)g.kp * g.dp * 2 + (size_t)nt * (g.dp + 4) * 4 + (size_t)g.kp * 4 + (size_t)nt * 4 +
-                     (s1_batched(sg.ns2) ? (size_t)S1_WAVES * S1_RING * (g.dp * 4 + 16 + 128) : 0);
+  const size_t lds = s1_lds_bytes(sg.ns2, sg.nb, !s1_table_global(sg.ns2, sg.nb));
   if (lds > 160 * 1024) return hipErrorInvalidValue;
+  (void)nt;
 #define KM_S1_CASE(NS2_, NB_)                                                                                   \
   case NS2_ * 100 + NB_:                                                                                        \
     if (delta)                                                                                                  \
@@ -1012,8 +1043,8 @@ hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, cons
     break;
   switch (sg.ns2 * 100 + sg.nb) {
     KM_S1_CASE(2, 2) KM_S1_CASE(2, 4) KM_S1_CASE(2, 6) KM_S1_CASE(2, 8)
-    KM_S1_CASE(1, 2) KM_S1_CASE(1, 4) KM_S1_CASE(1, 6) KM_S1_CASE(1, 8)
-    KM_S1_CASE(4, 2) KM_S1_CASE(4, 4)
+    KM_S1_CASE(1, 2) KM_S1_CASE(1, 4) KM_S1_CASE(1, 6) KM_S1_CASE(1, 8) KM_S1_CASE(1, 12) KM_S1_CASE(1, 16)
+    KM_S1_CASE(1, 32) KM_S1_CASE(2, 16) KM_S1_CASE(4, 2) KM_S1_CASE(4, 4)
     default:
       return hipErrorInvalidValue;
   }

@@ -209,7 +209,7 @@ def main():
 
     kern = {name: eng.prof_read(name) for name in ("assign", "resolve", "stats", "update", "prep")}
     info = eng.info()
-    screen = eng.screen() if info["fused_stats"] and info["path"] == 2 else None
+    screen = eng.screen() if info["path"] == 2 else None
     n_local = info["n"]
     flops_launch = 2.0 * n_local * k * d                 # algorithmic distance contraction
     bytes_stats = n_local * (d * 4 + 4)                  # X once + labels
@@ -250,18 +250,30 @@ def main():
     elif info["path"] == 2 and dom == "assign" and screen == 4:
         # k_s1 (km_screen1.hip): one fp16 MFMA per product (1.3 ms of MFMA at
         # c3 against 3.2 ms of HBM at the spec peak), candidates re-scored in
-        # fp32, delta statistics: bound by HBM, the rows read once
+        # fp32; delta statistics on the fused geometries (c3), labels only
+        # before the statistics pass on the unfused ones (c4)
         t_mfma = flops_launch / (F16_DENSE_TFLOPS * 1e12)
         b_alg = n_local * d * 4
         t_hbm = b_alg / (HBM_PEAK_GBS * 1e9)
-        ach = b_alg / avg_s / 1e9
-        roof = {"bound": "hbm" if t_hbm >= t_mfma else "mfma", "achieved": ach, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "k_s1 (one fp16 MFMA per product, fp32 re-score of candidates, delta statistics)",
-                "bytes_note": "algorithmic N*d*4 per launch (X read once, SURVEY 8d); the kernel also reads the "
-                              "previous label and the row-norm bound (8 B per row); MFMA time at one fp16 MFMA "
-                              f"per product {t_mfma * 1e3:.2f} ms vs {t_hbm * 1e3:.2f} ms HBM at 8 TB/s",
-                "tflops": flops_launch / avg_s / 1e12, "tflops_frac_f16_dense": flops_launch / avg_s / 1e12 / F16_DENSE_TFLOPS}
+        kname = ("k_s1 (one fp16 MFMA per product, fp32 re-score of candidates, delta statistics)"
+                 if info["fused_stats"] else
+                 "k_s1 (one fp16 MFMA per product, fp32 re-score of candidates; labels, statistics in a second pass)")
+        note = (f"MFMA time at one fp16 MFMA per product {t_mfma * 1e3:.2f} ms vs {t_hbm * 1e3:.2f} ms HBM at 8 TB/s; "
+                "the kernel also reads the row-norm bound (and, with delta statistics, the previous label): 4-8 B per row")
+        if t_hbm >= t_mfma:
+            ach = b_alg / avg_s / 1e9
+            roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                    "traffic": traffic, "kernel": kname,
+                    "bytes_note": "algorithmic N*d*4 per launch (X read once, SURVEY 8d); " + note,
+                    "tflops": flops_launch / avg_s / 1e12,
+                    "tflops_frac_f16_dense": flops_launch / avg_s / 1e12 / F16_DENSE_TFLOPS}
+        else:
+            ach = flops_launch / avg_s / 1e12
+            roof = {"bound": "mfma", "achieved": ach, "peak": F16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                    "frac": ach / F16_DENSE_TFLOPS, "traffic": traffic, "kernel": kname,
+                    "peak_note": "dense f16 MFMA 2516.6 TF, one MFMA per product; achieved = 2*n*k*d per launch / "
+                                 "avg launch time; " + note,
+                    "hbm_gbs": b_alg / avg_s / 1e9}
     elif info["path"] == 2 and dom == "assign":
         ach = flops_launch / avg_s / 1e12
         # the fused screen runs on v_mfma_f32_16x16x32_f16 where dp is a

@@ -107,6 +107,10 @@ def test_c3_class_selects_s1():
     (30000, 32, 250, 300),   # dp 32, kp 256 (8 members per chain, 1 MFMA k-slice)
     (20000, 128, 128, 128),  # dp 128, kp 128
     (20000, 64, 70, 40),     # kp 128, 58 pad slots
+    (20000, 32, 384, 200),   # dp 32, kp 384: 12 members per chain (run-time member loop)
+    (20000, 32, 512, 300),   # 16 members per chain
+    (20000, 32, 1024, 300),  # c4 shape: 32 members, fp32 table in global memory
+    (20000, 64, 512, 200),   # dp 64, kp 512: image 64 KiB, table in global memory
 ])
 def test_predict_blobs_vs_oracle(n, d, k, centers):
     X = _blobs(n, d, centers, seed=3 + d)
@@ -224,6 +228,7 @@ def test_fit_noise_delta_iterations():
     (30000, 32, 250, 300),
     (20000, 128, 128, 128),
     (20000, 64, 70, 40),
+    (20000, 32, 512, 300),
 ])
 def test_fit_shapes_delta_iterations(n, d, k, centers):
     X = _blobs(n, d, centers, seed=21 + k)
@@ -275,3 +280,33 @@ def test_compute_sse_keeps_full_statistics():
     ref = orc.lloyd_fit(X, 256, 3, 1e-12, 0, True, 1, init_centroids=C0, empty_seed=lambda: SEED)
     np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
     np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)
+
+
+# -- the unfused geometries (c4 class): k_s1 labels, then the statistics pass ------------
+
+@pytest.mark.parametrize("compute_sse", [True, False])
+def test_fit_c4_shape_labels_then_statistics_pass(compute_sse):
+    # k = 1024, d = 32 (c4's geometry; BASELINE configs[3] has compute_sse on):
+    # no fused statistics table fits, so k_s1 writes every label and the
+    # statistics pass (with the SSE residuals) reads X again; the delta table
+    # [k][d+1] f64 does not fit LDS either, so every iteration is full
+    X = _blobs(30000, 32, 1024, seed=61)
+    C0 = X[np.random.default_rng(62).choice(len(X), 1024, replace=False)]
+    km = _fit(X, C0, 4, compute_sse=compute_sse)
+    eng = km._runner.engine
+    assert eng.screen() == S1
+    ref = orc.lloyd_fit(X, 1024, 4, 1e-12, 0, compute_sse, 1, init_centroids=C0, empty_seed=lambda: SEED)
+    np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
+    if compute_sse:
+        np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)
+    C_prev = orc.lloyd_fit(X, 1024, 3, 1e-12, 0, False, 1, init_centroids=C0, empty_seed=lambda: SEED)["centroids"]
+    np.testing.assert_array_equal(eng.labels(), orc.assign(X, C_prev)[0])
+
+
+def test_c4_shape_forced_fp16x3_screen_still_available():
+    # km_set_screen(1) keeps the fp16x3 unfused screen on this geometry
+    X = _blobs(20000, 32, 1024, seed=63)
+    C = X[np.random.default_rng(64).choice(len(X), 1024, replace=False)]
+    a, eng = _predict(X, C, 1)
+    assert eng.screen() == 1
+    np.testing.assert_array_equal(a, orc.assign(X, C)[0])
