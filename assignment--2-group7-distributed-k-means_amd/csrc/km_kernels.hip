@@ -146,6 +146,23 @@ __host__ __device__ inline float screen_b0(float xn_s, float cm_s, float pm_s, i
   return fmaf(screen_slope(cm_s, dp, shape16), xn_s, screen_icpt(cm_s, pm_s, dp, shape16));
 }
 
+// The same bound for the one-MFMA screen (k_assign_mfma16<..., ONE>): the
+// image RN16(-2 s c') and the row RN16(s x) are single fp16 parts, so the
+// product error is (2 u16 + u16^2) |a||b| per feature (Cauchy-Schwarz:
+// 2 (2 u16 + u16^2) cm xn), fp16 subnormals add 2^-25 sqrt(dp) (xn + 2 cm)
+// (1 + u16), c vs c' 2 u cm xn, the norm u cm^2, and the 16x16x32
+// accumulation model of dp / 32 MFMAs per chain (4 u |D| and 28 u of the
+// largest product each), times 1.5 like screen_b0.
+__host__ __device__ inline float screen_b0_one(float xn_s, float cm_s, float pm_s, int dp) {
+  constexpr float U16 = 4.8828125e-04f;
+  const float nmf = (float)dp / 32.0f, sq = sqrtf((float)dp) * (1.0f + U16);
+  const float slope = (2.0f * U24 + 2.0f * (2.0f * U16 + U16 * U16) + 8.0f * nmf * U24) * cm_s +
+                      2.98023223876953125e-08f * sq;
+  const float icpt = (1.0f + 4.0f * nmf) * U24 * cm_s * cm_s + 56.2f * nmf * U24 * pm_s +
+                     5.9604644775390625e-08f * sq * cm_s;
+  return 1.5f * fmaf(slope, xn_s, icpt);
+}
+
 // Per-key screening bounds (scaled units), used where the global-cmax test
 // above cannot separate the candidates (e.g. far-away centroids inflate
 // cmax).  Every term of screen_b0 is a function of the candidate's own scaled
@@ -181,6 +198,20 @@ struct KeyBounds {
     return fmaxf(fminf(f, g) - 8.0f * U24 * (fabsf(km) + E + r * (r + 2.0f * x)), floor_);
   }
 };
+
+// E(r) of screen_b0_one (cm -> r, pm -> r min(xn, xabs))
+__device__ __forceinline__ KeyBounds key_bounds_one(float xn_s, float xabs_s, int dp, float rho) {
+  constexpr float U16 = 4.8828125e-04f;
+  const float nmf = (float)dp / 32.0f, sq = sqrtf((float)dp) * (1.0f + U16);
+  KeyBounds kb;
+  kb.e2 = 1.5f * U24 * (1.0f + 4.0f * nmf);
+  kb.e1 = 1.5f * ((2.0f * U24 + 2.0f * (2.0f * U16 + U16 * U16) + 8.0f * nmf * U24) * xn_s +
+                  56.2f * nmf * U24 * fminf(xn_s, xabs_s) + 5.9604644775390625e-08f * sq);
+  kb.e0 = 1.5f * 2.98023223876953125e-08f * sq * xn_s;
+  kb.x = xn_s;
+  kb.rho = rho * 1.01f + 2.0f * U24;
+  return kb;
+}
 
 // E(r) coefficients for a point of scaled norm bound xn_s (xabs_s: scaled
 // max |x_f| over the data), the terms of screen_b0 with the same 1.5 safety
@@ -761,6 +792,7 @@ struct MfmaArgs {
   uint32_t* cand;      // candidate pool (kind-4 entries): CAND_REC words per record, nullptr: off
   uint32_t* cand_ctr;  // records taken this launch (zeroed before it)
   uint32_t cand_cap;   // records
+  int one = 0;         // k_assign_mfma16: one fp16 MFMA per product (KM_SCREEN_ONE)
 };
 
 // LDS image of a centroid chunk: for block b (32 centroids) and K-step t the
@@ -1236,7 +1268,7 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
 // halves and merged over quarter pairs (as k_fused16), so lanes l and l ^ 16
 // own row (l & 15) + 16 (l >> 5).  The bound is screen_b0's 16x16x32 model.
 // ---------------------------------------------------------------------------
-template <int NS, int WAVES, bool T2 = false>
+template <int NS, int WAVES, bool T2 = false, bool ONE = false>
 __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_assign_mfma16(MfmaArgs A) {
   if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   static_assert(NS % 2 == 0, "dp a multiple of 32");
@@ -1283,7 +1315,7 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
     for (int id = threadIdx.x; id < npieces; id += WAVES * 64) {
       const size_t src = piece_src(id >> 6, id & 63);
       *reinterpret_cast<uint4*>(sHi + (size_t)id * 16) = *reinterpret_cast<const uint4*>(gh + src);
-      *reinterpret_cast<uint4*>(sLo + (size_t)id * 16) = *reinterpret_cast<const uint4*>(gl + src);
+      if constexpr (!ONE) *reinterpret_cast<uint4*>(sLo + (size_t)id * 16) = *reinterpret_cast<const uint4*>(gl + src);
     }
     for (int id = threadIdx.x; id < kc; id += WAVES * 64) sCn[id] = A.cn2s[(size_t)ch * KC + id];
   };
@@ -1299,8 +1331,9 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
       const size_t src = piece_src(pc, lane);
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(gh + src),
                                        (__attribute__((address_space(3))) void*)(dHi + (size_t)pc * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(gl + src),
-                                       (__attribute__((address_space(3))) void*)(dLo + (size_t)pc * 1024), 16, 0, 0);
+      if constexpr (!ONE)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(gl + src),
+                                         (__attribute__((address_space(3))) void*)(dLo + (size_t)pc * 1024), 16, 0, 0);
     }
     const char* gc = reinterpret_cast<const char*>(A.cn2s + (size_t)ch * KC);
     for (int pc = wave; pc * 1024 < kc * 4; pc += WAVES)
@@ -1390,18 +1423,20 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
       const size_t off = (size_t)blk * BLKB + (size_t)tt * 1024;
       Frag f;
       f.hi = *reinterpret_cast<const f16x8*>(laneHi + off);
-      f.lo = *reinterpret_cast<const f16x8*>(laneLo + off);
+      if constexpr (!ONE) f.lo = *reinterpret_cast<const f16x8*>(laneLo + off);
       return f;
     };
     // piece tt = cb NS2 + sl: the half cb's contribution of slab sl, both row groups
     auto mfma_step = [&](Acc& a, const Frag& f, int tt) {
       const int cb = tt / NS2, sl = tt - (tt / NS2) * NS2;
+      if constexpr (!ONE) {
 #pragma unroll
-      for (int pg = 0; pg < 2; ++pg)
-        a.v[cb][pg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.hi, bl[pg][sl], a.v[cb][pg], 0, 0, 0);
+        for (int pg = 0; pg < 2; ++pg)
+          a.v[cb][pg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.hi, bl[pg][sl], a.v[cb][pg], 0, 0, 0);
 #pragma unroll
-      for (int pg = 0; pg < 2; ++pg)
-        a.v[cb][pg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.lo, bh[pg][sl], a.v[cb][pg], 0, 0, 0);
+        for (int pg = 0; pg < 2; ++pg)
+          a.v[cb][pg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.lo, bh[pg][sl], a.v[cb][pg], 0, 0, 0);
+      }
 #pragma unroll
       for (int pg = 0; pg < 2; ++pg)
         a.v[cb][pg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.hi, bh[pg][sl], a.v[cb][pg], 0, 0, 0);
@@ -1546,7 +1581,7 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
       top3p_insert(k1, k2, k3, p1, p2, __uint_as_float(Q3), 0u);
     }
     const float xn = sqrtf(xx[pgo]) * 1.0001f;
-    const float B0 = screen_b0(xn, cm, pm, DP, 1);
+    const float B0 = ONE ? screen_b0_one(xn, cm, pm, DP) : screen_b0(xn, cm, pm, DP, 1);
     const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k3));
     const float thr2 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k2));
     uint32_t kind = 0;
@@ -1562,7 +1597,7 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
     }
     float u1 = FLT_MAX;
     if (__ballot(kind != 0u) != 0ull && kind != 0u) {
-      const KeyBounds kb = key_bounds(xn, *A.xabs * s, DP, rho, 1);
+      const KeyBounds kb = ONE ? key_bounds_one(xn, *A.xabs * s, DP, rho) : key_bounds(xn, *A.xabs * s, DP, rho, 1);
       u1 = kb.upper(k1);
       if (u1 < kb.lower(k2))
         kind = 0u;
@@ -1587,7 +1622,8 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
 #pragma unroll
       for (int pg = 0; pg < 2; ++pg) {
         act[pg] = kdo[pg] == 2u;
-        kbg[pg] = key_bounds(sqrtf(xx[pg]) * 1.0001f, *A.xabs * s, DP, rho, 1);
+        kbg[pg] = ONE ? key_bounds_one(sqrtf(xx[pg]) * 1.0001f, *A.xabs * s, DP, rho)
+                      : key_bounds(sqrtf(xx[pg]) * 1.0001f, *A.xabs * s, DP, rho, 1);
         const float K1 = __uint_as_float(k1o[pg]);
         over[pg] = act[pg] && (!(K1 == K1) || !(fabsf(K1) < 3.0e38f));
       }
@@ -1960,6 +1996,16 @@ static bool launch_mfma16_ns(int waves, int blocks, size_t lds, hipStream_t s, c
   } else {
     if (!on) return false;
     const bool t2 = mfma_top2(NS);
+    if (a.one) {
+      // one fp16 MFMA per product: the 12- / 8-wave instances
+      if (waves == 12)
+        hipLaunchKernelGGL((k_assign_mfma16<NS, 12, false, true>), dim3(blocks), dim3(768), lds, s, a);
+      else if (waves == 16 && NS <= 4)
+        hipLaunchKernelGGL((k_assign_mfma16<NS, 16, false, true>), dim3(blocks), dim3(1024), lds, s, a);
+      else
+        hipLaunchKernelGGL((k_assign_mfma16<NS, 8, false, true>), dim3(blocks), dim3(512), lds, s, a);
+      return true;
+    }
     if (waves == 16 && NS <= 4) {
       if (t2)
         hipLaunchKernelGGL((k_assign_mfma16<NS, 16, true>), dim3(blocks), dim3(1024), lds, s, a);
@@ -2048,7 +2094,7 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
                               const float* cn2s, const float* cmax, const float* xabs, const float* cabs,
                               int32_t* labels, QEntry* queue, uint32_t* qcount, int n_cu, QLayout* ql,
                               const int* gate, hipStream_t s, uint32_t* cand, uint32_t* cand_ctr,
-                              uint32_t cand_cap) {
+                              uint32_t cand_cap, int one) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
@@ -2086,7 +2132,7 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
     if (e != hipSuccess) return e;
   }
   MfmaArgs a{X, g.n, g.k, g.kp, KC, seg, Chi, Clo, cn2s, cmax, xabs, cabs, labels, queue, qcount, gate,
-             use_cand ? cand : nullptr, cand_ctr, cand_cap};
+             use_cand ? cand : nullptr, cand_ctr, cand_cap, (one && g.dp % 32 == 0 && g.dp <= 256) ? 1 : 0};
   switch (g.dp / 16) {
     case 1: launch_mfma_ns<1>(waves, nb, lds, s, a); break;
     case 2: launch_mfma_ns<2>(waves, nb, lds, s, a); break;

@@ -432,6 +432,14 @@ bool fold_ok(km_ctx* c) {
 
 int run_assign(km_ctx* c, bool with_stats);
 
+// the unfused screen with one fp16 MFMA per product (KM_SCREEN_ONE): forced,
+// or by default where k_s1 has no instance (dp a multiple of 32, <= 256)
+bool one_screen(km_ctx* c) {
+  if (c->path != 2 || c->fused || c->g.dp % 32 != 0 || c->g.dp > 256) return false;
+  if (c->screen_forced == KM_SCREEN_ONE) return true;
+  return c->screen_forced < 0 && !c->s1;
+}
+
 // k_s1 for this assign: labels only (predict), or delta statistics once the
 // labels and the full sums of a previous iteration are in place (no SSE: its
 // residuals need every row; and only where k_s1_delta's table fits LDS)
@@ -552,7 +560,7 @@ int run_assign(km_ctx* c, bool with_stats) {
     ProfScope ps(c, KM_K_ASSIGN);
     KM_HIP(km::launch_assign_mfma(c->X, g, c->Chi, c->Clo, c->cn2s, c->cmax, c->xabs, c->cabs, c->labels, c->queue,
                                   c->qcount, c->n_cu, &c->ql, c->gate, c->stream, c->cand, c->cand_ctr,
-                                  c->cand_cap));
+                                  c->cand_cap, one_screen(c) ? 1 : 0));
   }
   {
     ProfScope ps(c, KM_K_RESOLVE);
@@ -795,15 +803,15 @@ int km_sum_x(km_ctx* c, double* out) {
 
 int km_set_screen(km_ctx* c, int32_t mode) {
   KM_REQUIRE(c, KM_ERR_ARG, "null ctx");
-  KM_REQUIRE(mode >= -1 && mode <= KM_SCREEN_S1, KM_ERR_ARG, "km_set_screen: mode must be -1..4");
+  KM_REQUIRE(mode >= -1 && mode <= KM_SCREEN_ONE, KM_ERR_ARG, "km_set_screen: mode must be -1..5");
 #ifndef KM_DIAG
   // the fast screens (k_fused1) lost end to end on every BASELINE shape
   // (DESIGN.md "Fast screen"): built in the diagnostic library only
-  KM_REQUIRE(mode <= km::KM_SCREEN_X3_REFINE || mode == KM_SCREEN_S1, KM_ERR_UNSUPPORTED,
+  KM_REQUIRE(mode <= km::KM_SCREEN_X3_REFINE || mode == KM_SCREEN_S1 || mode == KM_SCREEN_ONE, KM_ERR_UNSUPPORTED,
              "km_set_screen: fast screens (modes 2, 3) are in the diagnostic build only");
 #endif
   c->screen_forced = mode;
-  if (mode >= 0 && mode != KM_SCREEN_S1) c->screen = mode;
+  if (mode >= 0 && mode != KM_SCREEN_S1 && mode != KM_SCREEN_ONE) c->screen = mode;
   return KM_OK;
 }
 
@@ -812,7 +820,7 @@ int km_get_screen(km_ctx* c, int32_t* mode) {
   // the screen of the next fused assign with statistics
   *mode = (use_s1(c, true) || (c->s1 && !c->fused && (c->screen_forced < 0 || c->screen_forced == KM_SCREEN_S1)))
               ? KM_SCREEN_S1
-              : c->screen;
+              : one_screen(c) ? KM_SCREEN_ONE : c->screen;
   return KM_OK;
 }
 

@@ -56,7 +56,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--screen", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4],
+    p.add_argument("--screen", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4, 5],
                    help="fused-path screen (km_set_screen): -1 the runtime's choice (4 = k_s1 where the "
                         "geometry has it), 0/1 fp16x3 k_fused16 with full statistics every iteration "
                         "(2, 3: diagnostic library only)")
@@ -274,6 +274,15 @@ def main():
                     "peak_note": "dense f16 MFMA 2516.6 TF, one MFMA per product; achieved = 2*n*k*d per launch / "
                                  "avg launch time; " + note,
                     "hbm_gbs": b_alg / avg_s / 1e9}
+    elif info["path"] == 2 and dom == "assign" and screen == 5:
+        # KM_SCREEN_ONE: k_assign_mfma16 with one fp16 MFMA per product
+        ach = flops_launch / avg_s / 1e12
+        roof = {"bound": "mfma", "achieved": ach, "peak": F16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / F16_DENSE_TFLOPS, "traffic": traffic,
+                "kernel": "k_assign_mfma16 (one fp16 MFMA per product on 16x16x32, one-part bound)",
+                "peak_note": "dense f16 MFMA 2516.6 TF, one MFMA per product; achieved = 2*n*k*d per launch / "
+                             "avg launch time (HIP events, engine stream)",
+                "hbm_gbs": n_local * d * 4 / avg_s / 1e9}
     elif info["path"] == 2 and dom == "assign":
         ach = flops_launch / avg_s / 1e12
         # the fused screen runs on v_mfma_f32_16x16x32_f16 where dp is a
@@ -345,8 +354,9 @@ def main():
             "screen": screen,
             "predict": pred,
             "arith": ("fp16 MFMA screen (balanced image, pairwise bound)" if screen in (2, 3) else
-                      "one fp16 MFMA per product, candidates re-scored in fp32 with a rigorous bound, float64 "
-                      "delta statistics" if screen == 4 else
+                      "one fp16 MFMA per product, candidates re-scored in fp32 with a rigorous bound" +
+                      (", float64 delta statistics" if info["fused_stats"] else "") if screen == 4 else
+                      "one fp16 MFMA per product with a rigorous one-part bound" if screen == 5 else
                       "fp16x3 MFMA screen with a rigorous bound") +
                      ", float64 exact re-rank of ambiguous points, float64 partial sums",
         }

@@ -215,23 +215,28 @@ int km_predict(km_ctx* ctx, int32_t* labels_out);
 /* Labels of the last km_assign_stats (device -> host). */
 int km_labels(km_ctx* ctx, int32_t* labels_out);
 
-/* Screening kernel of the fused path (k = 256, d <= 64 class).  A cost
- * choice: labels, sums and SSE are exact in every mode.  -1 (default): the
- * one-MFMA screen (mode 4) wherever the geometry has an instance, else per
- * batch from the last iteration's queue fraction; 0: fp16x3 screen, global
- * bound; 1: fp16x3 with per-key bounds (0 and 1 keep k_fused16 with full
- * statistics on every iteration); 4 (ABI 5): one fp16 MFMA per product,
- * candidates re-scored exactly in fp32 inside the kernel, delta statistics
- * (the first iteration after new data, centroids or a predict still runs
- * the fp16x3 screen with full statistics; with compute_sse every iteration
- * does).  Modes 2 and 3 (fast screen: one fp16 MFMA per product, pairwise
- * bound; 3 with the row split hi + lo) exist in the diagnostic library only
- * (libkmeans_amd_diag.so, make diag); the product library returns
- * KM_ERR_UNSUPPORTED for them. */
+/* Screening kernel.  A cost choice: labels, sums and SSE are exact in every
+ * mode.  -1 (default): the one-MFMA screen k_s1 (mode 4) wherever the
+ * geometry has an instance, else mode 5 on the unfused path (dp a multiple
+ * of 32), else per batch from the last iteration's queue fraction; 0: fp16x3
+ * screen, global bound; 1: fp16x3 with per-key bounds (0 and 1 keep
+ * k_fused16 with full statistics on every iteration, and the fp16x3
+ * k_assign_mfma16 on the unfused path); 4 (ABI 5): k_s1, one fp16 MFMA per
+ * product, candidates re-scored exactly in fp32 inside the kernel, delta
+ * statistics on the fused geometries (the first iteration after new data,
+ * centroids or a predict still runs the fp16x3 screen with full statistics;
+ * with compute_sse every iteration does), labels then the statistics pass on
+ * the unfused ones; 5 (ABI 5): one fp16 MFMA per product in the unfused
+ * k_assign_mfma16 with the one-part bound, the rows it cannot settle going
+ * to the float64 resolvers (candidate lists).  Modes 2 and 3 (fast screen:
+ * one fp16 MFMA per product, pairwise bound; 3 with the row split hi + lo)
+ * exist in the diagnostic library only (libkmeans_amd_diag.so, make diag);
+ * the product library returns KM_ERR_UNSUPPORTED for them. */
 #define KM_SCREEN_AUTO (-1)
 #define KM_SCREEN_S1 4
+#define KM_SCREEN_ONE 5
 int km_set_screen(km_ctx* ctx, int32_t mode);
-/* The screen the next fused assign with statistics uses (0..4). */
+/* The screen the next assign with statistics uses (0..5). */
 int km_get_screen(km_ctx* ctx, int32_t* mode);
 
 /* Kernel timing with HIP events on the context stream.  `enable` is a

@@ -310,3 +310,35 @@ def test_c4_shape_forced_fp16x3_screen_still_available():
     a, eng = _predict(X, C, 1)
     assert eng.screen() == 1
     np.testing.assert_array_equal(a, orc.assign(X, C)[0])
+
+
+# -- KM_SCREEN_ONE: one fp16 MFMA per product in the unfused k_assign_mfma16 -------------
+
+ONE = 5  # KM_SCREEN_ONE (include/kmeans_amd.h)
+
+
+@pytest.mark.parametrize("n,d,k,centers", [
+    (8000, 128, 4096, 512),   # c5 geometry: chunked images, top-2 chains (dp 128)
+    (12000, 64, 1536, 300),   # dp 64, chunked, top-3 chains
+    (12000, 96, 640, 200),    # dp 96 (not a multiple of 32): the fp16x3 32x32x16 screen stays
+])
+def test_one_mfma_unfused_screen_predict_vs_oracle(n, d, k, centers):
+    X = _blobs(n, d, centers, seed=70 + d)
+    C = X[np.random.default_rng(71).choice(n, k, replace=False)]
+    a, eng = _predict(X, C)
+    np.testing.assert_array_equal(a, orc.assign(X, C)[0])
+    assert eng.screen() == (ONE if d % 32 == 0 else 1)
+    b, _ = _predict(X, C, 1)
+    np.testing.assert_array_equal(a, b)
+
+
+def test_one_mfma_unfused_screen_fit_c5_shape():
+    # the c5 geometry (d 128, k 4096) through fit: labels, then the sorted
+    # statistics pass; centroids and SSE against the oracle
+    X = _blobs(12000, 128, 1024, seed=81)
+    C0 = X[np.random.default_rng(82).choice(len(X), 4096, replace=False)]
+    km = _fit(X, C0, 3, compute_sse=True)
+    assert km._runner.engine.screen() == ONE
+    ref = orc.lloyd_fit(X, 4096, 3, 1e-12, 0, True, 1, init_centroids=C0, empty_seed=lambda: SEED)
+    np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)
