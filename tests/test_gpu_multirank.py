@@ -98,3 +98,69 @@ def test_two_ranks_on_gpu_match_reference(golden, name):
         if name in ("empty", "c5_poor"):
             assert reps > 0, "the empty clusters were not repaired on the device"
     assert res[0][4] and not res[1][4]  # only rank 0 logs
+
+
+def _rank_delta(rank, world, port, q):
+    # c3 geometry (d 64, k 256), compute_sse off: from the second iteration
+    # every rank runs k_s1 with delta statistics, and the all-reduce sums the
+    # ranks' deltas, which k_s1_apply folds into each rank's copy of the full
+    # sums (the same on every rank: they were all-reduced too)
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import kmeans_amd as ka
+        X, C0 = _delta_data()
+
+        class Pinned(ka.KMeans):
+            def _initialize_centroids(self, run):
+                return C0.copy()
+
+            def _empty_seed(self):
+                return 1234
+
+        km = Pinned(k=len(C0), max_iter=6, tolerance=1e-12, compute_sse=False)
+        km.verbose = False
+        km.fit(X)
+        eng = km._runner.engine
+        q.put((rank, km.centroids, eng.screen(), km._runner.last["counts"].copy(), km._runner.iterations_run
+               if hasattr(km._runner, "iterations_run") else None))
+    except Exception as e:  # surface the failure in the parent
+        q.put((rank, repr(e), None, None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _delta_data():
+    rng = np.random.default_rng(91)
+    C = rng.uniform(-10, 10, (256, 64))
+    X = (C[rng.integers(0, 256, 40000)] + rng.standard_normal((40000, 64))).astype(np.float32).astype(np.float64)
+    C0 = X[np.random.default_rng(92).choice(len(X), 256, replace=False)]
+    return X, C0
+
+
+def test_two_ranks_delta_statistics_c3_shape():
+    import torch.multiprocessing as mp
+    from oracle import kmeans_oracle as orc
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_delta, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=110) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0, res
+    X, C0 = _delta_data()
+    ref = orc.lloyd_fit(X, 256, 6, 1e-12, 0, False, 1, init_centroids=C0, empty_seed=lambda: 1234)
+    for rank, C, screen, counts, _ in res:
+        assert screen == 4, "k_s1 (delta statistics) not selected"
+        np.testing.assert_allclose(C, ref["centroids"], rtol=1e-9, atol=1e-9)
+        assert int(counts.sum()) == len(X)
