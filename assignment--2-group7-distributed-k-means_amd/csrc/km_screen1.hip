@@ -78,6 +78,12 @@ constexpr int S1_RING = 16;                     // rows per re-scoring batch (on
 // the re-scoring batches run where a wave's ring (S1_RING rows of DP floats,
 // 16 B of row data and 128 B of chain heads) fits beside the tables: dp <= 64
 constexpr bool s1_batched(int ns2) { return ns2 <= 2; }
+// tiles of 16 rows per wave step (A/B knob for 32-wide rows: two tiles per
+// step lost at c4 on one box, 230 vs 159-169 ms)
+#ifndef KM_S1_TT
+#define KM_S1_TT 1
+#endif
+constexpr int s1_tiles(int ns2) { return ns2 == 1 ? KM_S1_TT : 1; }
 
 // k_s1's LDS: image, fp32 table (unless it goes to global), norms, slots,
 // re-scoring rings; the table goes to global memory where all of it would
@@ -532,114 +538,11 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     }
   };
 
-  auto process = [&](uint32_t tile, const Buf& B) {
+  // everything after the chains of one tile: certificate, labels, queue,
+  // re-scoring ring
+  auto tail = [&](uint32_t tile, const Buf& B, const float (&h)[2][4], const float (&h2)[2][4]) {
     const uint32_t row = tile * 16u + (uint32_t)c16;
     const bool valid = row < n;
-    // B operands: RN16(s x), features FQ q + 8 t .. + 8 of slice t
-    f16x8 bx[NS2];
-#pragma unroll
-    for (int t = 0; t < NS2; ++t) {
-      const float4 a = B.x[2 * t], c = B.x[2 * t + 1];
-      bx[t][0] = (_Float16)(a.x * s);
-      bx[t][1] = (_Float16)(a.y * s);
-      bx[t][2] = (_Float16)(a.z * s);
-      bx[t][3] = (_Float16)(a.w * s);
-      bx[t][4] = (_Float16)(c.x * s);
-      bx[t][5] = (_Float16)(c.y * s);
-      bx[t][6] = (_Float16)(c.z * s);
-      bx[t][7] = (_Float16)(c.w * s);
-    }
-    // this lane's 8 chains: best key (head, member id in the low MB bits)
-    // and second key
-    float h[2][4], h2[2][4];
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) h[cb][i] = h2[cb][i] = FLT_MAX;
-    const float4* cnl = reinterpret_cast<const float4*>(sCn + 4 * q);  // + 8 blk + 4 cb
-    // a block pair's operands from LDS: A fragments (lane-linear 1 KiB
-    // pieces, conflict-free) and accumulator inits; the next pair's are
-    // read while this pair's MFMAs and key updates run
-    struct Pair {
-      f16x8 a[2][2][NS2];  // [block of the pair][cb][t]
-      float4 c[2][2];      // [block of the pair][cb]
-    };
-    auto load_pair = [&](int blk, Pair& P) {
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          P.c[e][cb] = cnl[8 * (blk + e) + 4 * cb];
-#pragma unroll
-          for (int t = 0; t < NS2; ++t)
-            P.a[e][cb][t] = __builtin_bit_cast(f16x8, sImg[(((blk + e) * 2 + cb) * NS2 + t) * 64 + lane]);
-        }
-    };
-    Pair pr[2];
-    load_pair(0, pr[0]);
-    // blocks in pairs: two members per step, new best = min3(best, ka, kb),
-    // new second = min(second, med3(best, ka, kb))
-    auto mfma_pair = [&](const Pair& P, f32x4 (&a)[2][2]) {
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb) a[e][cb] = f32x4{P.c[e][cb].x, P.c[e][cb].y, P.c[e][cb].z, P.c[e][cb].w};
-#pragma unroll
-      for (int t = 0; t < NS2; ++t)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-          for (int e = 0; e < 2; ++e)
-            a[e][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(P.a[e][cb][t], bx[t], a[e][cb], 0, 0, 0);
-    };
-    auto keys_pair = [&](int blk, const f32x4 (&a)[2][2]) {
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float ka = u2f((f2u(a[0][cb][i]) & KMASK) | (uint32_t)blk);
-          const float kb = u2f((f2u(a[1][cb][i]) & KMASK) | (uint32_t)(blk + 1));
-          const float t = __builtin_amdgcn_fmed3f(h[cb][i], ka, kb);
-          h[cb][i] = __builtin_fminf(__builtin_fminf(h[cb][i], ka), kb);
-          h2[cb][i] = __builtin_fminf(h2[cb][i], t);
-        }
-    };
-    // one block pair in flight (plus the next one's operands): the scheduler
-    // would otherwise hoist every pair's reads and MFMAs ahead of the key
-    // updates; the partner wave on the SIMD fills the MFMA pipe while this one
-    // updates its keys
-    if constexpr (NB <= 8) {
-#pragma unroll
-      for (int blk = 0; blk < NB; blk += 2) {
-        const Pair& P = pr[(blk >> 1) & 1];
-        if (blk + 2 < NB) load_pair(blk + 2, pr[((blk >> 1) + 1) & 1]);
-        f32x4 a[2][2];
-        mfma_pair(P, a);
-        keys_pair(blk, a);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {
-      // many members (NB a multiple of 4): two pairs per trip of a loop, the
-      // member id a run-time value
-      static_assert(NB % 4 == 0, "NB > 8 must be a multiple of 4");
-#pragma unroll 1
-      for (int blk = 0; blk < NB; blk += 4) {
-        load_pair(blk + 2, pr[1]);
-        {
-          f32x4 a[2][2];
-          mfma_pair(pr[0], a);
-          keys_pair(blk, a);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (blk + 4 < NB) load_pair(blk + 4, pr[0]);
-        {
-          f32x4 a[2][2];
-          mfma_pair(pr[1], a);
-          keys_pair(blk + 2, a);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
     // full slot ids in the heads, (chain << MB) | member: distinct keys, so
     // float comparisons order them totally (f32 denormals are kept, and +0
     // and -0 could only share a slot); non-finite rows are caught by `bad`
@@ -778,24 +681,140 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     }
   };
 
-  // this wave's tiles gw, gw + nw, ...: two register buffers, the next
-  // tile's loads in flight while one is processed (loads past the end read
-  // row n - 1 and are never used)
-  // NBUF register buffers of rows: NBUF - 1 tiles' loads in flight while
-  // one is processed (short rows need more of them to keep HBM busy)
-  constexpr int NBUF = KM_S1_NBUF > 0 ? KM_S1_NBUF : (NS2 == 1 ? 4 : 2);
-  Buf b[NBUF];
+  // TT tiles of 16 rows per wave step (two where rows are 32 wide: the
+  // block pairs' image reads and their latency are shared by twice the rows)
+  constexpr int TT = s1_tiles(NS2);
+  auto process = [&](uint32_t st, const Buf (&BB)[TT]) {
+    // B operands: RN16(s x), features FQ q + 8 t .. + 8 of slice t
+    f16x8 bx[TT][NS2];
 #pragma unroll
-  for (int u = 0; u + 1 < NBUF; ++u) load(gw + (uint32_t)u * nw, b[u]);
-  // (tile + 2 NBUF nw stays below 2^32: ntiles < 2^28, nw < 2^16)
-  for (uint32_t tile = gw; tile < ntiles; tile += (uint32_t)NBUF * nw) {
+    for (int u = 0; u < TT; ++u)
+#pragma unroll
+      for (int t = 0; t < NS2; ++t) {
+        const float4 a = BB[u].x[2 * t], c = BB[u].x[2 * t + 1];
+        bx[u][t][0] = (_Float16)(a.x * s);
+        bx[u][t][1] = (_Float16)(a.y * s);
+        bx[u][t][2] = (_Float16)(a.z * s);
+        bx[u][t][3] = (_Float16)(a.w * s);
+        bx[u][t][4] = (_Float16)(c.x * s);
+        bx[u][t][5] = (_Float16)(c.y * s);
+        bx[u][t][6] = (_Float16)(c.z * s);
+        bx[u][t][7] = (_Float16)(c.w * s);
+      }
+    // this lane's 8 chains per tile: best key (head, member id in the low MB
+    // bits) and second key
+    float h[TT][2][4], h2[TT][2][4];
+#pragma unroll
+    for (int u = 0; u < TT; ++u)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[u][cb][i] = h2[u][cb][i] = FLT_MAX;
+    const float4* cnl = reinterpret_cast<const float4*>(sCn + 4 * q);  // + 8 blk + 4 cb
+    // a block pair's operands from LDS: A fragments (lane-linear 1 KiB
+    // pieces, conflict-free) and accumulator inits; the next pair's are
+    // read while this pair's MFMAs and key updates run
+    struct Pair {
+      f16x8 a[2][2][NS2];  // [block of the pair][cb][t]
+      float4 c[2][2];      // [block of the pair][cb]
+    };
+    auto load_pair = [&](int blk, Pair& P) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          P.c[e][cb] = cnl[8 * (blk + e) + 4 * cb];
+#pragma unroll
+          for (int t = 0; t < NS2; ++t)
+            P.a[e][cb][t] = __builtin_bit_cast(f16x8, sImg[(((blk + e) * 2 + cb) * NS2 + t) * 64 + lane]);
+        }
+    };
+    Pair pr[2];
+    load_pair(0, pr[0]);
+    // blocks in pairs: two members per step, new best = min3(best, ka, kb),
+    // new second = min(second, med3(best, ka, kb))
+    auto step = [&](int blk, const Pair& P) {
+      f32x4 a[TT][2][2];
+#pragma unroll
+      for (int u = 0; u < TT; ++u)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+            a[u][e][cb] = f32x4{P.c[e][cb].x, P.c[e][cb].y, P.c[e][cb].z, P.c[e][cb].w};
+#pragma unroll
+      for (int t = 0; t < NS2; ++t)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int u = 0; u < TT; ++u)
+              a[u][e][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(P.a[e][cb][t], bx[u][t], a[u][e][cb], 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < TT; ++u)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float ka = u2f((f2u(a[u][0][cb][i]) & KMASK) | (uint32_t)blk);
+            const float kb = u2f((f2u(a[u][1][cb][i]) & KMASK) | (uint32_t)(blk + 1));
+            const float t = __builtin_amdgcn_fmed3f(h[u][cb][i], ka, kb);
+            h[u][cb][i] = __builtin_fminf(__builtin_fminf(h[u][cb][i], ka), kb);
+            h2[u][cb][i] = __builtin_fminf(h2[u][cb][i], t);
+          }
+    };
+    // one block pair in flight (plus the next one's operands): the scheduler
+    // would otherwise hoist every pair's reads and MFMAs ahead of the key
+    // updates; the partner wave on the SIMD fills the MFMA pipe while this one
+    // updates its keys
+    if constexpr (NB <= 8) {
+#pragma unroll
+      for (int blk = 0; blk < NB; blk += 2) {
+        const Pair& P = pr[(blk >> 1) & 1];
+        if (blk + 2 < NB) load_pair(blk + 2, pr[((blk >> 1) + 1) & 1]);
+        step(blk, P);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+      // many members (NB a multiple of 4): two pairs per trip of a loop, the
+      // member id a run-time value
+      static_assert(NB % 4 == 0, "NB > 8 must be a multiple of 4");
+#pragma unroll 1
+      for (int blk = 0; blk < NB; blk += 4) {
+        load_pair(blk + 2, pr[1]);
+        step(blk, pr[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (blk + 4 < NB) load_pair(blk + 4, pr[0]);
+        step(blk + 2, pr[1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < TT; ++u) tail(st * TT + (uint32_t)u, BB[u], h[u], h2[u]);
+  };
+
+  // this wave's steps gw, gw + nw, ... of TT tiles each; NBUF register
+  // buffers of rows: NBUF - 1 steps' loads in flight while one is processed
+  // (loads past the end read row n - 1 and are never used)
+  constexpr int NBUF = KM_S1_NBUF > 0 ? KM_S1_NBUF : (NS2 == 1 && NB > 8 ? 3 : 2);
+  const uint32_t nst = (ntiles + (uint32_t)TT - 1u) / (uint32_t)TT;
+  Buf b[NBUF][TT];
+  auto load_step = [&](uint32_t st, Buf (&BB)[TT]) {
+#pragma unroll
+    for (int u = 0; u < TT; ++u) load(st * TT + (uint32_t)u, BB[u]);
+  };
+#pragma unroll
+  for (int u = 0; u + 1 < NBUF; ++u) load_step(gw + (uint32_t)u * nw, b[u]);
+  // (st + 2 NBUF nw stays below 2^32: ntiles < 2^28, nw < 2^16)
+  for (uint32_t st = gw; st < nst; st += (uint32_t)NBUF * nw) {
     bool done = false;
 #pragma unroll
     for (int u = 0; u < NBUF; ++u) {
       if (!done) {
-        load(tile + (uint32_t)(u + NBUF - 1) * nw, b[(u + NBUF - 1) % NBUF]);
-        process(tile + (uint32_t)u * nw, b[u]);
-        done = tile + (uint32_t)(u + 1) * nw >= ntiles;
+        load_step(st + (uint32_t)(u + NBUF - 1) * nw, b[(u + NBUF - 1) % NBUF]);
+        process(st + (uint32_t)u * nw, b[u]);
+        done = st + (uint32_t)(u + 1) * nw >= nst;
       }
     }
     if (done) break;
@@ -915,12 +934,13 @@ __global__ __launch_bounds__(1024) void k_s1_delta(const float* __restrict__ X, 
 // k_s1's grid: workgroups (one per CU at most, 8 waves each) and the rows
 // of one wave's queue / change-list segment
 static int64_t s1_grid(const Geometry& g, int n_cu, int* nbk, uint32_t* seg) {
-  const int64_t ntiles = (g.n + 15) / 16;
+  const int tt = s1_tiles(g.dp / 32);
+  const int64_t nst = ((g.n + 15) / 16 + tt - 1) / tt;  // wave steps of tt tiles
   int64_t blocks = n_cu;
-  if (blocks > (ntiles + S1_WAVES - 1) / S1_WAVES) blocks = (ntiles + S1_WAVES - 1) / S1_WAVES;
+  if (blocks > (nst + S1_WAVES - 1) / S1_WAVES) blocks = (nst + S1_WAVES - 1) / S1_WAVES;
   *nbk = (int)blocks;
   const int64_t nw = blocks * S1_WAVES;
-  *seg = nw ? (uint32_t)(((ntiles + nw - 1) / nw) * 16) : 0u;
+  *seg = nw ? (uint32_t)(((nst + nw - 1) / nw) * 16 * tt) : 0u;
   return nw;
 }
 
