@@ -83,6 +83,9 @@ constexpr bool s1_batched(int ns2) { return ns2 <= 2; }
 #ifndef KM_S1_TT
 #define KM_S1_TT 1
 #endif
+#ifndef KM_S1_QUAD
+#define KM_S1_QUAD 0  // A/B knob: key updates four members at a time
+#endif
 constexpr int s1_tiles(int ns2) { return ns2 == 1 ? KM_S1_TT : 1; }
 
 // k_s1's LDS: image, fp32 table (unless it goes to global), norms, slots,
@@ -509,18 +512,18 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
       for (int u = 0; u < FQ / 4; ++u) xv[u] = xs[u];
       const uint32_t cnt = mt.y >> 16;
       uint32_t sl[S1_LMAX];
-      sl[0] = mt.z & 0xFFFFu;
-      sl[1] = mt.z >> 16;
+      sl[0] = mt.z;
 #pragma unroll
-      for (int r = 2; r < S1_LMAX; ++r) sl[r] = 0u;
-      if (__ballot(act && cnt >= 3u) != 0ull) {
-        // candidates 3, 4, ...: the row's smallest heads above the second
+      for (int r = 1; r < S1_LMAX; ++r) sl[r] = 0u;
+      {
+        // candidates 2, 3, ...: the row's smallest heads above the first
+        // (every row here has at least two)
         const float4* hp = sRh + ((wave * S1_RING + slot) * 4 + q) * 2;
         const float4 h0 = hp[0], h1 = hp[1];
         const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
         float prev = u2f(mt.w);
 #pragma unroll
-        for (int r = 2; r < S1_LMAX; ++r) {
+        for (int r = 1; r < S1_LMAX; ++r) {
           if (__ballot(act && (uint32_t)r < cnt) == 0ull) break;
           float nl = FLT_MAX;
 #pragma unroll
@@ -556,20 +559,27 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
         __builtin_fminf(__builtin_fminf(h2[0][0], h2[0][1]), __builtin_fminf(h2[0][2], h2[0][3])),
         __builtin_fminf(__builtin_fminf(h2[1][0], h2[1][1]), __builtin_fminf(h2[1][2], h2[1][3])));
 
-    // the row's two smallest heads (m and the second candidate), then the
-    // candidate threshold T: the lane's lowest two (med3 keeps the middle of
-    // a sorted pair and a new value), merged over the quad
+    // the row's smallest head m, then the candidate threshold T (the
+    // batched re-score finds the other candidates from the stored heads; the
+    // in-tile one of dp > 64 takes the second smallest head here: the lane's
+    // lowest two, med3 keeping the middle of a sorted pair and a new value,
+    // merged over the quad)
     auto mn = [](float a, float b) { return __builtin_fminf(a, b); };
     auto mx = [](float a, float b) { return __builtin_fmaxf(a, b); };
     float la = FLT_MAX, lb = FLT_MAX;
+    if constexpr (BATCH) {
+      la = __builtin_fminf(
+          __builtin_fminf(__builtin_fminf(hk[0][0], hk[0][1]), __builtin_fminf(hk[0][2], hk[0][3])),
+          __builtin_fminf(__builtin_fminf(hk[1][0], hk[1][1]), __builtin_fminf(hk[1][2], hk[1][3])));
+      la = quad_min(la);
+    } else {
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
+      for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        lb = __builtin_amdgcn_fmed3f(la, lb, hk[cb][i]);  // (la <= lb)
-        la = mn(la, hk[cb][i]);
-      }
-    {
+        for (int i = 0; i < 4; ++i) {
+          lb = __builtin_amdgcn_fmed3f(la, lb, hk[cb][i]);  // (la <= lb)
+          la = mn(la, hk[cb][i]);
+        }
       auto p = __builtin_amdgcn_permlane16_swap(f2u(la), f2u(la), false, false);
       auto p2 = __builtin_amdgcn_permlane16_swap(f2u(lb), f2u(lb), false, false);
       float a0 = u2f(p[0]), a1 = u2f(p[1]), b0 = u2f(p2[0]), b1 = u2f(p2[1]);
@@ -625,27 +635,24 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
 #endif
     if constexpr (BATCH) {
       emit(valid && !needy, row, dec1 ? 0u : 2u, labm, 0, old);
-      // rows with 2..LMAX candidates: into the wave's ring with their two
-      // smallest heads' slots (and, for 3 or more candidates, every chain
-      // head, from which the batch extracts the rest); a full ring is
-      // re-scored as one batch
+      // rows with 2..LMAX candidates: into the wave's ring with their
+      // smallest head and every chain head, from which the batch extracts the
+      // rest; a full ring is re-scored as one batch
       const uint64_t mrow = __ballot(needy && q == 0);
       if (mrow) {
         const uint32_t nn = (uint32_t)__popcll(mrow);
         const uint32_t rk = (uint32_t)__popcll(mrow & ((1ull << c16) - 1ull));
         const uint32_t space = (uint32_t)S1_RING - rc;
-        const uint4 meta = make_uint4(row, (uint32_t)old | (cnt << 16), sm | ((f2u(lb) & SLOTM) << 16), f2u(lb));
+        const uint4 meta = make_uint4(row, (uint32_t)old | (cnt << 16), sm, f2u(la));
         auto stash = [&](uint32_t slot) {
           float4* xs = reinterpret_cast<float4*>(sRx + (wave * S1_RING + slot) * DP + FQ * q);
 #pragma unroll
           for (int u = 0; u < FQ / 4; ++u) xs[u] = B.x[u];
           if (q == 0) sRm[wave * S1_RING + slot] = meta;
-          // the heads only matter with 3 or more candidates
-          if (cnt >= 3u) {
-            float4* hp = sRh + ((wave * S1_RING + slot) * 4 + q) * 2;
-            hp[0] = make_float4(hk[0][0], hk[0][1], hk[0][2], hk[0][3]);
-            hp[1] = make_float4(hk[1][0], hk[1][1], hk[1][2], hk[1][3]);
-          }
+          // the chain heads: the batch extracts candidates 2, 3, ... from them
+          float4* hp = sRh + ((wave * S1_RING + slot) * 4 + q) * 2;
+          hp[0] = make_float4(hk[0][0], hk[0][1], hk[0][2], hk[0][3]);
+          hp[1] = make_float4(hk[1][0], hk[1][1], hk[1][2], hk[1][3]);
         };
         if (needy && rk < space) stash(rc + rk);
         if (nn >= space) {
@@ -768,7 +775,48 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     // would otherwise hoist every pair's reads and MFMAs ahead of the key
     // updates; the partner wave on the SIMD fills the MFMA pipe while this one
     // updates its keys
-    if constexpr (NB <= 8) {
+    if constexpr (KM_S1_QUAD && TT == 1 && NB <= 8 && NB % 4 == 0) {
+      // A/B knob: keys of four members at a time, 9 operations per four keys
+      // instead of 10 (two pairs' accumulators live together)
+      auto mfma_only = [&](const Pair& P, f32x4 (&a)[2][2]) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) a[e][cb] = f32x4{P.c[e][cb].x, P.c[e][cb].y, P.c[e][cb].z, P.c[e][cb].w};
+#pragma unroll
+        for (int t = 0; t < NS2; ++t)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+              a[e][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(P.a[e][cb][t], bx[0][t], a[e][cb], 0, 0, 0);
+      };
+#pragma unroll
+      for (int blk = 0; blk < NB; blk += 4) {
+        f32x4 a[2][2], b2[2][2];
+        load_pair(blk + 2, pr[1]);
+        mfma_only(pr[0], a);
+        __builtin_amdgcn_sched_barrier(0);
+        if (blk + 4 < NB) load_pair(blk + 4, pr[0]);
+        mfma_only(pr[1], b2);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float ka = u2f((f2u(a[0][cb][i]) & KMASK) | (uint32_t)blk);
+            const float kb = u2f((f2u(a[1][cb][i]) & KMASK) | (uint32_t)(blk + 1));
+            const float kc = u2f((f2u(b2[0][cb][i]) & KMASK) | (uint32_t)(blk + 2));
+            const float kd = u2f((f2u(b2[1][cb][i]) & KMASK) | (uint32_t)(blk + 3));
+            float& hh = h[0][cb][i];
+            const float s1v = __builtin_amdgcn_fmed3f(hh, ka, kb);
+            const float m1 = __builtin_fminf(__builtin_fminf(hh, ka), kb);
+            const float s2v = __builtin_amdgcn_fmed3f(m1, kc, kd);
+            hh = __builtin_fminf(__builtin_fminf(m1, kc), kd);
+            h2[0][cb][i] = __builtin_fminf(__builtin_fminf(h2[0][cb][i], s1v), s2v);
+          }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (NB <= 8) {
 #pragma unroll
       for (int blk = 0; blk < NB; blk += 2) {
         const Pair& P = pr[(blk >> 1) & 1];
