@@ -121,7 +121,8 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
                               const float* cn2s, const float* cmax, const float* xabs, const float* cabs,
                               int32_t* labels, QEntry* queue, uint32_t* qcount, int n_cu, QLayout* ql,
                               const int* gate, hipStream_t s, uint32_t* cand = nullptr, uint32_t* cand_ctr = nullptr,
-                              uint32_t cand_cap = 0, int one = 0);
+                              uint32_t cand_cap = 0, int one = 0,
+                              const float* C32 = nullptr);
 int cand_rec_words();
 // queue capacity (entries) and per-wave counter words needed for n rows
 size_t queue_capacity(int64_t n, int n_cu);

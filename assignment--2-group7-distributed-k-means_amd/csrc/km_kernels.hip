@@ -793,6 +793,7 @@ struct MfmaArgs {
   uint32_t* cand_ctr;  // records taken this launch (zeroed before it)
   uint32_t cand_cap;   // records
   int one = 0;         // k_assign_mfma16: one fp16 MFMA per product (KM_SCREEN_ONE)
+  const float* C32 = nullptr;  // ONE: fp32 centroids [kp][dp], the in-kernel pair re-score
 };
 
 // LDS image of a centroid chunk: for block b (32 centroids) and K-step t the
@@ -1604,6 +1605,59 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
       else if (kind == 2u && !same_chain && kb.lower(k3) > u1)
         kind = 1u;
     }
+    if constexpr (ONE) {
+      // The one-part bound leaves many pairs to the float64 re-rank (13% of
+      // c5 rows): re-score the pair in fp32 here first.  The two owner lanes
+      // of a row take half of its features each; bounds of ||x - c||
+      // (unscaled): |Dt - D'| <= (dp/2 + 4) u D' for the lane sums and their
+      // sum, sqrt(D') = r (1 +- (dp/4 + 2 + 4) u) with v_sqrt_f32 (2 ulp),
+      // widened by 8 u, and ||x - c|| = sqrt(D') +- u cmax (c vs its fp32 c').
+      // Below 2^-96 the hardware sqrt loses accuracy: U takes sqrt(2^-96),
+      // L takes 0.  Decided when one candidate's upper bound is below the
+      // other's lower bound; otherwise the pair stays for k_rerank2.
+      if (A.C32 != nullptr && __ballot(kind == 1u && valid) != 0ull) {
+        const bool act = kind == 1u && valid;
+        constexpr int HF = DP / 2;  // features per owner lane
+        const int hb = (q & 1) * HF;
+        const float4* xr = reinterpret_cast<const float4*>(A.X + (size_t)(act ? row : 0) * DP + hb);
+        const float4* c1 = reinterpret_cast<const float4*>(A.C32 + (size_t)(act ? p1 : 0) * DP + hb);
+        const float4* c2 = reinterpret_cast<const float4*>(A.C32 + (size_t)(act ? p2 : 0) * DP + hb);
+        float d1 = 0.0f, d2 = 0.0f;
+#pragma unroll 1
+        for (int u = 0; u < HF / 4; ++u) {
+          const float4 xv = xr[u], a = c1[u], b = c2[u];
+          float t;
+          t = xv.x - a.x; d1 = fmaf(t, t, d1);
+          t = xv.y - a.y; d1 = fmaf(t, t, d1);
+          t = xv.z - a.z; d1 = fmaf(t, t, d1);
+          t = xv.w - a.w; d1 = fmaf(t, t, d1);
+          t = xv.x - b.x; d2 = fmaf(t, t, d2);
+          t = xv.y - b.y; d2 = fmaf(t, t, d2);
+          t = xv.z - b.z; d2 = fmaf(t, t, d2);
+          t = xv.w - b.w; d2 = fmaf(t, t, d2);
+        }
+        // the partner lane (l ^ 16) holds the other half; the same order of
+        // addition in both (lower half first)
+        const float o1 = __shfl_xor(d1, 16), o2 = __shfl_xor(d2, 16);
+        const float D1 = (q & 1) ? o1 + d1 : d1 + o1;
+        const float D2 = (q & 1) ? o2 + d2 : d2 + o2;
+        constexpr float EPS = (float)(DP / 4 + 14) * U24;
+        const float gm = U24 * *A.cmax * 1.01f + 1e-37f;
+        auto ub = [&](float D) {
+          const float r = __builtin_amdgcn_sqrtf(D >= 0x1p-96f ? D : 0x1p-96f);
+          return fmaf(r, 1.0f + EPS, gm) * (1.0f + 4.0f * U24);
+        };
+        auto lb = [&](float D) {
+          const float r = D >= 0x1p-96f ? __builtin_amdgcn_sqrtf(D) : 0.0f;
+          return fmaf(r, 1.0f - EPS, -gm) * (1.0f - 4.0f * U24);
+        };
+        const float U1 = ub(D1), L1 = lb(D1), U2 = ub(D2), L2 = lb(D2);
+        const bool win1 = act && L2 > U1, win2 = act && L1 > U2;
+        // (select form: DESIGN.md section 2)
+        p1 = win2 ? p2 : p1;
+        kind = (win1 || win2) ? 0u : kind;
+      }
+    }
     // Candidate lists (kind 4), as in k_assign_mfma: the row's 16 chains
     // are spread over the four quarter lanes of its column, each holding
     // them for both row groups; every lane lists the kept keys of its own
@@ -2094,7 +2148,7 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
                               const float* cn2s, const float* cmax, const float* xabs, const float* cabs,
                               int32_t* labels, QEntry* queue, uint32_t* qcount, int n_cu, QLayout* ql,
                               const int* gate, hipStream_t s, uint32_t* cand, uint32_t* cand_ctr,
-                              uint32_t cand_cap, int one) {
+                              uint32_t cand_cap, int one, const float* C32) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
@@ -2132,7 +2186,7 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
     if (e != hipSuccess) return e;
   }
   MfmaArgs a{X, g.n, g.k, g.kp, KC, seg, Chi, Clo, cn2s, cmax, xabs, cabs, labels, queue, qcount, gate,
-             use_cand ? cand : nullptr, cand_ctr, cand_cap, (one && g.dp % 32 == 0 && g.dp <= 256) ? 1 : 0};
+             use_cand ? cand : nullptr, cand_ctr, cand_cap, (one && g.dp % 32 == 0 && g.dp <= 256) ? 1 : 0, C32};
   switch (g.dp / 16) {
     case 1: launch_mfma_ns<1>(waves, nb, lds, s, a); break;
     case 2: launch_mfma_ns<2>(waves, nb, lds, s, a); break;

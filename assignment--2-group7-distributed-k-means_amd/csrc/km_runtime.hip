@@ -432,6 +432,12 @@ bool fold_ok(km_ctx* c) {
 
 int run_assign(km_ctx* c, bool with_stats);
 
+// the one-MFMA unfused screen re-scores its pairs in fp32 in the kernel (A/B
+// knob: 0 leaves them all to k_rerank2)
+#ifndef KM_PAIR_RESCORE
+#define KM_PAIR_RESCORE 1
+#endif
+
 // the unfused screen with one fp16 MFMA per product (KM_SCREEN_ONE): forced,
 // or by default where k_s1 has no instance (dp a multiple of 32, <= 256)
 bool one_screen(km_ctx* c) {
@@ -560,7 +566,7 @@ int run_assign(km_ctx* c, bool with_stats) {
     ProfScope ps(c, KM_K_ASSIGN);
     KM_HIP(km::launch_assign_mfma(c->X, g, c->Chi, c->Clo, c->cn2s, c->cmax, c->xabs, c->cabs, c->labels, c->queue,
                                   c->qcount, c->n_cu, &c->ql, c->gate, c->stream, c->cand, c->cand_ctr,
-                                  c->cand_cap, one_screen(c) ? 1 : 0));
+                                  c->cand_cap, one_screen(c) ? 1 : 0, KM_PAIR_RESCORE ? c->C32 : nullptr));
   }
   {
     ProfScope ps(c, KM_K_RESOLVE);
