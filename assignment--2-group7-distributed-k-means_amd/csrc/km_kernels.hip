@@ -3939,12 +3939,17 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
     // most batches hold chain scans only: skip the chunk pass unless some
     // wave of the workgroup still has a full scan
     if (!__syncthreads_or(any_full)) continue;
-    if constexpr (WIDE) {
-      // wide rows (no LDS room for a chunk): lane j reads C64T straight
-      // from L2, consecutive centroids on consecutive lanes
+    // (reading C64T straight from L2 for short queues as well, instead of
+    // staging chunks through LDS, doubled the c3 resolve time on one box:
+    // 0.069 -> 0.137 ms; only the wide rows do it)
+    constexpr bool direct = WIDE;
+    if (direct) {
+      // lane j reads C64T straight from L2, consecutive centroids on
+      // consecutive lanes
       static_assert(G == 2 || G == 4, "entries per wave");
       auto direct = [&](int j, const float* xg, double& bst, int& bjj) {
-        const double v = np_norm_d<5>([&](int f) { return np_sq(C64T[(size_t)f * k + j], xg[f]); }, d);
+        const double v = WIDE ? np_norm_d<5>([&](int f) { return np_sq(C64T[(size_t)f * k + j], xg[f]); }, d)
+                              : np_norm_d<2>([&](int f) { return np_sq(C64T[(size_t)f * k + j], xg[f]); }, d);
         const bool u = np_better(v, bst, bjj >= 0);  // select form
         bst = u ? v : bst;
         bjj = u ? j : bjj;
@@ -3958,7 +3963,7 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
         }
       }
     }
-    for (int c0 = 0; !WIDE && c0 < k; c0 += ch) {
+    for (int c0 = 0; !direct && c0 < k; c0 += ch) {
       __syncthreads();  // the previous chunk is consumed (and the rows staged)
       const int cw = min(ch, k - c0);
       for (int i = threadIdx.x; i < d * ch; i += blockDim.x) {

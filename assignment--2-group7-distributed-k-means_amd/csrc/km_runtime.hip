@@ -456,15 +456,24 @@ bool use_s1(km_ctx* c, bool with_stats) {
 }
 
 // before an update reads the statistics: delta -> fold into the full sums;
-// full -> keep them as the base of the next deltas
-int apply_stats(km_ctx* c) {
+// full -> keep them as the base of the next deltas.  Returns the buffer the
+// update reads: with `clear` (an update that leaves its input alone) the
+// folded sums stay in stats_full and the deltas are zeroed for the next
+// iteration (no memset before it); else stats = the folded sums.
+int apply_stats(km_ctx* c, const double** upd_src = nullptr, bool clear = false) {
   const int kind = c->stats_pending;
   c->stats_pending = 0;
+  if (upd_src) *upd_src = c->stats;
   if (!c->s1) return KM_OK;
   const bool keep = kind == 2 || (kind == 1 && !c->want_sse);
+  const bool zero = kind == 2 && clear && upd_src;
   if (keep)
-    KM_HIP(km::launch_s1_apply(c->stats, c->stats_full, (int64_t)stats_len(c->g), kind == 2 ? 1 : 0, c->gate,
-                               c->stream));
+    KM_HIP(km::launch_s1_apply(c->stats, c->stats_full, (int64_t)stats_len(c->g), kind == 2 ? (zero ? 2 : 1) : 0,
+                               c->gate, c->stream));
+  if (zero) {
+    *upd_src = c->stats_full;
+    c->stats_clean = true;  // the deltas are zero for the next assign
+  }
   c->delta_ready = keep;
   return KM_OK;
 }
@@ -1011,13 +1020,14 @@ int km_update(km_ctx* c, km_status* st, int64_t* counts) {
     const int rcf = flush_assign(c);
     if (rcf != KM_OK) return rcf;
   }
+  const double* src = nullptr;
   {
-    const int rca = apply_stats(c);
+    const int rca = apply_stats(c, &src, !km::update_one_ok(c->g));
     if (rca != KM_OK) return rca;
   }
   {
     ProfScope ps(c, KM_K_UPDATE);
-    KM_HIP(km::launch_update(c->stats, c->C64_cur, c->g, c->C64_new, c->work, c->counts_dev, c->qcount,
+    KM_HIP(km::launch_update(const_cast<double*>(src), c->C64_cur, c->g, c->C64_new, c->work, c->counts_dev, c->qcount,
                              c->ql.nwaves, c->status_dev, c->gate, -1.0, 0, c->stream));
   }
   KM_HIP(hipMemcpyAsync(c->status_host, c->status_dev, sizeof(km::DevStatus), hipMemcpyDeviceToHost, c->stream));
@@ -1152,13 +1162,15 @@ int km_update_async(km_ctx* c, double tol, int64_t empty_seed) {
     c->stats_clean = true;  // the update cleared them
     return finish_update(c, slot, fold_prep);
   }
+  const double* src = nullptr;
   {
-    const int rca = apply_stats(c);
+    // (k_update_one clears its input: it reads the folded sums in stats)
+    const int rca = apply_stats(c, &src, !one);
     if (rca != KM_OK) return rca;
   }
   {
     ProfScope ps(c, KM_K_UPDATE);
-    KM_HIP(km::launch_update(c->stats, c->C64_cur, c->g, c->C64_new, c->work,
+    KM_HIP(km::launch_update(one ? c->stats : const_cast<double*>(src), c->C64_cur, c->g, c->C64_new, c->work,
                              c->hist_counts + (size_t)slot * c->g.k, c->qcount, c->ql.nwaves, c->hist + slot,
                              c->gate, tol, repair ? 1 : 0, c->stream, one ? 1 : 0, fold_prep ? c->C32 : nullptr,
                              fold_prep ? c->cmax : nullptr));

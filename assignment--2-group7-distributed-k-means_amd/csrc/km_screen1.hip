@@ -877,17 +877,19 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
 
 // Delta statistics (km_runtime.hip): mode 1 folds an iteration's all-reduced
 // deltas into the full sums and hands them to the update (full += stats;
-// stats = full); mode 0 keeps an iteration's full statistics (full = stats),
-// the base of the next deltas.  The SSE slot rides along (0 in delta mode).
+// stats = full); mode 2 folds them and clears the deltas for the next
+// iteration (full += stats; stats = 0: the update reads full, no memset);
+// mode 0 keeps an iteration's full statistics (full = stats), the base of
+// the next deltas.  The SSE slot rides along (0 in delta mode).
 __global__ __launch_bounds__(256) void k_s1_apply(double* __restrict__ stats, double* __restrict__ full, int64_t len,
                                                   int mode, const int* __restrict__ gate) {
   if (*gate) return;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= len) return;
   double v = stats[i];
-  if (mode == 1) v = full[i] + v;
+  if (mode >= 1) v = full[i] + v;
   full[i] = v;
-  stats[i] = v;
+  stats[i] = mode == 2 ? 0.0 : v;
 }
 
 // The change list of k_s1 into the delta statistics.  The list is nw wave
@@ -898,7 +900,10 @@ __global__ __launch_bounds__(256) void k_s1_apply(double* __restrict__ stats, do
 // old cluster to its new one in an LDS float64 table [k][d+1] (lanes over
 // features: consecutive banks), 8 rows per wave in flight, then adds the
 // table's non-zero entries to the statistics with global atomics.
-constexpr uint32_t S1D_MIN = 2048;
+#ifndef KM_S1D_MIN
+#define KM_S1D_MIN 256
+#endif
+constexpr uint32_t S1D_MIN = KM_S1D_MIN;
 constexpr int S1D_ROWS = 8;
 __global__ __launch_bounds__(1024) void k_s1_delta(const float* __restrict__ X, int dp, int d, int k,
                                                    const uint2* __restrict__ chg, const uint32_t* __restrict__ cnt,
