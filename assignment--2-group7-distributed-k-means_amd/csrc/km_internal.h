@@ -107,6 +107,7 @@ struct SmallTail {
   float* cmaxn;
   int kp;
   uint32_t* qout = nullptr;  // no fold: the queued-row count for the update's status (qcount[0..1])
+  int rev = 0;  // sweep the rows from the last one down (alternate launches: the Infinity Cache holds the previous sweep's tail)
 };
 hipError_t launch_assign_small(const float* X, const Geometry& g, const float* C32, const double* C64,
                                const float* cmax, int32_t* labels, double* stats, int fuse_stats, int want_sse,

@@ -353,6 +353,26 @@ __device__ void update_one_body(double* __restrict__ stats, const double* __rest
 #ifndef KM_SMALL_WPE
 #define KM_SMALL_WPE 4
 #endif
+// A/B knobs, c2 on one MI355X (profiles/r5_c2_small_ab.json):
+//   KM_SMALL_SERP serpentine sweep: 153-155 -> 145 us (6,450 -> 6,840 it/s)
+//   KM_SMALL_SC   centroids as scalar operands: 141-142 -> 135-136 us
+//   KM_SMALL_PF2  two rows prefetched (4 waves): +4-5 us, off
+//   KM_SMALL_PF8  the one-row prefetch at 6 waves per SIMD: +5 us, off
+#ifndef KM_SMALL_PF2
+#define KM_SMALL_PF2 0
+#endif
+#ifndef KM_SMALL_SC
+#define KM_SMALL_SC 1
+#endif
+#ifndef KM_SMALL_PF8
+#define KM_SMALL_PF8 0
+#endif
+#ifndef KM_SMALL_SERP
+#define KM_SMALL_SERP 1
+#endif
+#ifndef KM_SMALL_ABL  // timing ablations only (wrong sums): 1 no global flush, 2 no statistics at all
+#define KM_SMALL_ABL 0
+#endif
 template <int DP, bool SSE, int WPE = (DP <= 16 ? KM_SMALL_WPE : 1)>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const float* __restrict__ C32,
@@ -371,7 +391,8 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
   double* tab = reinterpret_cast<double*>(smem + ((k * DP * 4 + 15) / 16) * 16);
   const int d1 = d + 1;
   const int lane = threadIdx.x & 63;
-  for (int i = threadIdx.x; i < k * DP; i += blockDim.x) sC[i] = C32[i];
+  if (!KM_SMALL_SC)
+    for (int i = threadIdx.x; i < k * DP; i += blockDim.x) sC[i] = C32[i];
   if (fuse)
     for (int i = threadIdx.x; i < k * d1 * R; i += blockDim.x) tab[i] = 0.0;
   __syncthreads();
@@ -396,12 +417,22 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
   uint32_t wq_n = 0;
   // PF: the next row prefetched into registers while this one is processed
   // (at 8 waves per SIMD the other waves hide the latency instead: no
-  // prefetch, 2 dp fewer VGPRs)
-  constexpr bool PF = WPE < 8;
-  float4 nx[DP / 4];
+  // prefetch, 2 dp fewer VGPRs); PF2: two rows ahead (KM_SMALL_PF2)
+  constexpr bool PF = WPE < 8 || KM_SMALL_PF8;
+  constexpr bool PF2 = PF && KM_SMALL_PF2 && DP <= 16;
+  // serpentine sweep: every other launch visits the rows from the last one
+  // down, so its first ~200 MB are the previous launch's last reads, still in
+  // the 256 MiB Infinity Cache (same rows, same per-row work; only the order)
+  const bool rev = KM_SMALL_SERP && T.rev;
+  auto at = [&](int64_t v) { return rev ? n - 1 - v : v; };
+  float4 nx[DP / 4], nx2[DP / 4];
   if (PF && row < n) {
 #pragma unroll
-    for (int f = 0; f < DP; f += 4) nx[f / 4] = *reinterpret_cast<const float4*>(X + row * DP + f);
+    for (int f = 0; f < DP; f += 4) nx[f / 4] = *reinterpret_cast<const float4*>(X + at(row) * DP + f);
+  }
+  if (PF2 && row + rstride < n) {
+#pragma unroll
+    for (int f = 0; f < DP; f += 4) nx2[f / 4] = *reinterpret_cast<const float4*>(X + at(row + rstride) * DP + f);
   }
   auto row_body = [&](const float (&x)[DP], int64_t row) {
     float k1 = FLT_MAX, k2 = FLT_MAX, k3 = FLT_MAX;
@@ -413,7 +444,9 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
       // direct-form bound (DP sequential terms) covers two sums of DP / 2
 #pragma unroll 2
       for (int j = 0; j < k; ++j) {
-        const f32x2* c2 = reinterpret_cast<const f32x2*>(sC + j * DP);
+        // KM_SMALL_SC: the centroid through uniform (scalar) loads from C32,
+        // operands from SGPRs, instead of LDS reads into VGPRs
+        const f32x2* c2 = reinterpret_cast<const f32x2*>((KM_SMALL_SC ? C32 : sC) + j * DP);
         f32x2 acc2 = {0.0f, 0.0f};
 #pragma unroll
         for (int f = 0; f < DP; f += 2) {
@@ -461,7 +494,7 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
         }
       sacc += r;
     }
-    if (fuse) {
+    if (fuse && KM_SMALL_ABL < 2) {
       double* t = tab + (size_t)lab * d1 * R + rep;
 #pragma unroll
       for (int f = 0; f < DP; ++f)
@@ -482,17 +515,30 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
 #pragma unroll
     for (int f = 0; f < DP; f += 4) v[f / 4] = *reinterpret_cast<const float4*>(X + r * DP + f);
   };
-  for (; row < n; row += rstride) {
-    float x[DP];
-    if constexpr (PF) {
+  if constexpr (PF2) {
+    for (; row < n; row += 2 * rstride) {
+      float x[DP];
       unpack(nx, x);
-      if (row + rstride < n) load_row(nx, row + rstride);
-    } else {
-      float4 v[DP / 4];
-      load_row(v, row);
-      unpack(v, x);
+      if (row + 2 * rstride < n) load_row(nx, at(row + 2 * rstride));
+      row_body(x, at(row));
+      if (row + rstride >= n) break;
+      unpack(nx2, x);
+      if (row + 3 * rstride < n) load_row(nx2, at(row + 3 * rstride));
+      row_body(x, at(row + rstride));
     }
-    row_body(x, row);
+  } else {
+    for (; row < n; row += rstride) {
+      float x[DP];
+      if constexpr (PF) {
+        unpack(nx, x);
+        if (row + rstride < n) load_row(nx, at(row + rstride));
+      } else {
+        float4 v[DP / 4];
+        load_row(v, at(row));
+        unpack(v, x);
+      }
+      row_body(x, at(row));
+    }
   }
   // A queued row, resolved by one wave, lanes over centroids: the
   // reference's float64 norms (kmeans_spark.py:153) in NumPy's pairwise
@@ -568,7 +614,7 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
     for (int e = threadIdx.x; e < k * d1; e += blockDim.x) {
       double s = 0.0;
       for (int r = 0; r < R; ++r) s += tab[(size_t)e * R + r];
-      if (s != 0.0) atomicAdd(stats + e, s);
+      if (s != 0.0 && KM_SMALL_ABL == 0) atomicAdd(stats + e, s);
     }
   }
   // ---- the last workgroup: queued rows, then (fold) the update ----
@@ -582,6 +628,8 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
   __shared__ int s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  // (one ticket per workgroup on one counter; per-group counters and 16
+  // copies of the sums, merged by the last workgroup, measured 7% slower)
   if (threadIdx.x == 0)
     s_last = __hip_atomic_fetch_add(T.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
   __syncthreads();

@@ -104,6 +104,8 @@ struct km_ctx {
   uint2* chg = nullptr;          // k_s1 change list, one segment per wave, {row, old << 16 | new}
   uint32_t* chg_cnt = nullptr;   // entries per wave segment (written by every delta k_s1)
   bool delta_ready = false;      // labels and stats_full describe one assignment
+  bool x3_stale = true;          // Chi/Clo/cn2s/bnd not made for the prepared centroids (ensure_x3)
+  bool sweep_rev = false;        // small path: the last launch swept the rows downwards
   int stats_pending = 0;         // the last assign left 0 nothing, 1 full sums, 2 deltas in stats
   float* bal = nullptr;  // fast screen: image error maxima (2 floats)
   // statistics already zero (the batch update cleared them): no memset
@@ -331,6 +333,16 @@ void free_data(km_ctx* c) {
 // derived images (fp32 copy, transposed f64, fp16 hi/lo split, norms, bound
 // constants) of centroid buffer `src` (C64_cur, or C64_new speculatively in
 // km_update so the next iteration's assign starts right after the host sync)
+// the fp16 hi/lo split of the prepared centroid images and the screen's
+// bound constants (k_fused16 / k_assign_mfma16 inputs)
+int ensure_x3(km_ctx* c) {
+  if (!c->x3_stale) return KM_OK;
+  KM_HIP(km::launch_prep_split(c->C32, c->g, c->cn2, c->xabs, c->cabs, c->Chi, c->Clo, c->cn2s, c->gate, c->stream));
+  KM_HIP(km::launch_bound_consts(c->cmax, c->xabs, c->cabs, c->g, c->bnd, c->gate, c->stream));
+  c->x3_stale = false;
+  return KM_OK;
+}
+
 int prep(km_ctx* c, const double* src) {
   ProfScope ps(c, KM_K_PREP);
   c->prep_of = src;
@@ -340,8 +352,13 @@ int prep(km_ctx* c, const double* src) {
   }
   KM_HIP(km::launch_prep_centroids(src, c->g, c->C32, c->cn2, c->cmax, c->cabs, c->C64T, c->C64P, c->gate,
                                    c->stream));
-  KM_HIP(km::launch_prep_split(c->C32, c->g, c->cn2, c->xabs, c->cabs, c->Chi, c->Clo, c->cn2s, c->gate, c->stream));
-  KM_HIP(km::launch_bound_consts(c->cmax, c->xabs, c->cabs, c->g, c->bnd, c->gate, c->stream));
+  // the fp16x3 images and screen bounds: k_s1 (and its resolvers) never
+  // read them, so with it they are made on first use (ensure_x3)
+  c->x3_stale = true;
+  if (!c->s1) {
+    const int rc = ensure_x3(c);
+    if (rc != KM_OK) return rc;
+  }
   if (c->s1) {
     if (c->s1_recolor) {
       KM_HIP(km::launch_s1_color(c->C32, c->g, c->s1_perm, c->gate, c->stream));
@@ -419,6 +436,7 @@ km::SmallTail small_tail(km_ctx* c) {
   t.done = c->small_ctr + 1;
   t.kp = c->g.kp;
   t.qout = c->qcount;
+  t.rev = c->sweep_rev = !c->sweep_rev;  // alternate the sweep direction per launch
   return t;
 }
 
@@ -531,6 +549,10 @@ int run_assign(km_ctx* c, bool with_stats) {
   }
   if (c->fused) {
     {
+      const int rc = ensure_x3(c);
+      if (rc != KM_OK) return rc;
+    }
+    {
       ProfScope ps(c, KM_K_ASSIGN, true);
       KM_HIP(km::launch_fused(c->X, c->xnorm, g, c->Chi, c->Clo, c->ChiF, c->CloF, c->cn2s, c->bnd, c->xabs, c->cabs,
                               c->labels, c->queue, c->qcount, c->stats, with_stats ? 1 : 0,
@@ -570,6 +592,10 @@ int run_assign(km_ctx* c, bool with_stats) {
     KM_HIP(hipMalloc(&c->cand, sizeof(uint32_t) * km::cand_rec_words() * (size_t)cap));
     KM_HIP(hipMalloc(&c->cand_ctr, sizeof(uint32_t)));
     c->cand_cap = (uint32_t)cap;
+  }
+  {
+    const int rc = ensure_x3(c);
+    if (rc != KM_OK) return rc;
   }
   {
     ProfScope ps(c, KM_K_ASSIGN);
