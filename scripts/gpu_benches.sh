@@ -6,7 +6,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-benches}; mkdir -p $OUT
 for spec in ${SPECS:-"c2|" "c4|" "c5|--predict 3" "c5_poor|--predict 3"}; do
-  CFG=${spec%%|*}; ARGS=${spec#*|}
+  CFG=${spec%%|*}; ARGS=${spec#*|}; ARGS=${ARGS//,/ }  # SPECS from the environment: commas for spaces
   timeout -k 10 400 python -u bench.py --config $CFG --no-cpu-baseline $ARGS > $OUT/bench_$CFG.json 2> $OUT/bench_$CFG.err || { echo "bench $CFG failed"; tail -5 $OUT/bench_$CFG.err; exit 1; }
   python3 -c "import json;d=json.load(open('$OUT/bench_$CFG.json'));print('$CFG', round(d['value'],3), round(d['ms_per_step'],3), {k:round(v,3) for k,v in d['kernel_avg_ms'].items()}, d['roofline']['kernel'][:40], (d.get('predict') or {}).get('kernel_ms'))"
 done
