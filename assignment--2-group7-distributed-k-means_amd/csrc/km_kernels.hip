@@ -358,6 +358,7 @@ __device__ void update_one_body(double* __restrict__ stats, const double* __rest
 //   KM_SMALL_SC   centroids as scalar operands: 141-142 -> 135-136 us
 //   KM_SMALL_PF2  two rows prefetched (4 waves): +4-5 us, off
 //   KM_SMALL_PF8  the one-row prefetch at 6 waves per SIMD: +5 us, off
+//   KM_SMALL_NTL  non-temporal label stores: -1 us; 32 statistics replicas +5 us
 #ifndef KM_SMALL_PF2
 #define KM_SMALL_PF2 0
 #endif
@@ -369,6 +370,9 @@ __device__ void update_one_body(double* __restrict__ stats, const double* __rest
 #endif
 #ifndef KM_SMALL_SERP
 #define KM_SMALL_SERP 1
+#endif
+#ifndef KM_SMALL_NTL  // labels stored non-temporal: +1% (the 40 MB of labels leave the cache to X)
+#define KM_SMALL_NTL 1
 #endif
 #ifndef KM_SMALL_ABL  // timing ablations only (wrong sums): 1 no global flush, 2 no statistics at all
 #define KM_SMALL_ABL 0
@@ -464,7 +468,12 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
     if (lab >= k) lab = 0;  // only reachable with non-finite data (np.argmin of NaNs -> 0)
     // a queued row's label is written by the last workgroup only (two
     // writers of one label in one launch could reach memory in either order)
-    if (!amb) labels[row] = lab;
+    if (!amb) {
+      if (KM_SMALL_NTL)
+        __builtin_nontemporal_store(lab, labels + row);  // keep the Infinity Cache for X (serpentine sweep)
+      else
+        labels[row] = lab;
+    }
     const uint64_t qm = __ballot(amb);
     if (qm) {  // rare: the wave's own LDS queue, past SMALL_QW rows the launch's queue
       const uint32_t pos = wq_n + (uint32_t)__popcll(qm & ((1ull << lane) - 1ull));
