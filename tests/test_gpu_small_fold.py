@@ -123,3 +123,39 @@ def test_flush_points_between_assign_and_update(between):
     np.testing.assert_allclose(recs[0][0].sse, ref["sse_history"][0], rtol=1e-9)
     np.testing.assert_array_equal(eng.labels(), orc.assign(X, C0)[0])
     np.testing.assert_allclose(eng.get_centroids(1), ref["centroids"], rtol=1e-9, atol=1e-12)
+
+
+def test_serpentine_sweeps_agree():
+    # k_assign_small sweeps the rows last-first on every other launch (the
+    # Infinity Cache then serves the previous sweep's tail): two consecutive
+    # launches on the same centroids, one in each direction, must give the
+    # oracle's labels, identical counts and sums equal up to float64
+    # summation order
+    import torch
+    X, C0 = _tie_data(n=1_000_000)
+    k, d = C0.shape
+    eng = _engine()
+    eng.load_host(X.astype(np.float32))
+    eng.set_sse(True)
+    eng.set_centroids(C0)
+    keep = torch.zeros(k * (d + 1) + 1, dtype=torch.float64, device="cuda:0")
+    torch.cuda.synchronize()
+    assert eng.lib.km_bind_stats_buffer(eng.ctx, ctypes.c_void_p(keep.data_ptr())) == 0
+    ref_labels, ref_mind, _ = orc.assign(X, C0)
+    outs = []
+    for _ in range(2):
+        eng.assign_stats()
+        eng.sync()
+        outs.append((eng.labels(), keep.cpu().numpy().copy()))
+    (la, sa), (lb, sb) = outs
+    np.testing.assert_array_equal(la, ref_labels)
+    np.testing.assert_array_equal(lb, ref_labels)
+    t_a, t_b = sa[:-1].reshape(k, d + 1), sb[:-1].reshape(k, d + 1)
+    np.testing.assert_array_equal(t_a[:, d], t_b[:, d])
+    np.testing.assert_array_equal(t_a[:, d], np.bincount(ref_labels, minlength=k))
+    np.testing.assert_allclose(t_b[:, :d], t_a[:, :d], rtol=1e-12, atol=1e-9)
+    sums = np.zeros((k, d))
+    np.add.at(sums, ref_labels, X)
+    np.testing.assert_allclose(t_a[:, :d], sums, rtol=1e-9, atol=1e-6)
+    np.testing.assert_allclose([sa[-1], sb[-1]], (ref_mind ** 2).sum(), rtol=1e-9)
+    del keep
