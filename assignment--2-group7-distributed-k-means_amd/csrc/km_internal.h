@@ -238,7 +238,7 @@ hipError_t launch_s1_prep(const double* C64, const float* C32, const Geometry& g
 hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, const uint4* img, const float* cn2o,
                      const float* cft, const int32_t* perm, const float* cst, int32_t* labels,
                      QEntry* queue, uint32_t* qcount, uint2* chg, uint32_t* chg_cnt, int delta, int n_cu,
-                     QLayout* ql, const int* gate, hipStream_t s);
+                     QLayout* ql, const int* gate, hipStream_t s, int rev = 0);
 // k_s1's change list: entries (wave segments) and per-wave counts to allocate
 size_t s1_chg_entries(const Geometry& g, int n_cu);
 size_t s1_wave_slots(int n_cu);

@@ -80,6 +80,9 @@ constexpr int S1_RING = 16;                     // rows per re-scoring batch (on
 constexpr bool s1_batched(int ns2) { return ns2 <= 2; }
 // tiles of 16 rows per wave step (A/B knob for 32-wide rows: two tiles per
 // step lost at c4 on one box, 230 vs 159-169 ms)
+#ifndef KM_S1_SERP  // serpentine sweeps of the delta fit on the (2, 8) geometry (c3 class; km_runtime next_sweep)
+#define KM_S1_SERP 1
+#endif
 #ifndef KM_S1_TT
 #define KM_S1_TT 1
 #endif
@@ -306,7 +309,7 @@ struct S1Args {
 // rows' by the resolvers).  MODE 1: delta statistics (the previous labels are
 // read; only changed labels are written and moved in the sums; queued rows
 // keep their previous label for the resolvers to compare).
-template <int NS2, int NB, int MODE>
+template <int NS2, int NB, int MODE, bool REV = false>
 __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
   if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   constexpr int DP = 32 * NS2;
@@ -368,8 +371,12 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     float xn;
     int32_t old;
   };
+  // serpentine sweep (REV: its own instance, since a run-time select in the
+  // row arithmetic cost the issue-bound c3 kernel 1.5%): step tiles mapped
+  // last-first; tiles past the end stay past the end
+  auto tmap = [&](uint32_t t) { return (REV && t < ntiles) ? ntiles - 1u - t : t; };
   auto load = [&](uint32_t tile, Buf& B) {
-    const uint32_t row = tile * 16u + (uint32_t)c16;
+    const uint32_t row = tmap(tile) * 16u + (uint32_t)c16;
     const uint32_t rr = row < n ? row : (n - 1u);
     const float4* xr = reinterpret_cast<const float4*>(A.X + (size_t)rr * DP + FQ * q);
 #pragma unroll
@@ -544,7 +551,7 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
   // everything after the chains of one tile: certificate, labels, queue,
   // re-scoring ring
   auto tail = [&](uint32_t tile, const Buf& B, const float (&h)[2][4], const float (&h2)[2][4]) {
-    const uint32_t row = tile * 16u + (uint32_t)c16;
+    const uint32_t row = tmap(tile) * 16u + (uint32_t)c16;
     const bool valid = row < n;
     // full slot ids in the heads, (chain << MB) | member: distinct keys, so
     // float comparisons order them totally (f32 denormals are kept, and +0
@@ -1092,7 +1099,7 @@ hipError_t launch_s1_prep(const double* C64, const float* C32, const Geometry& g
 hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, const uint4* img, const float* cn2o,
                      const float* cft, const int32_t* perm, const float* cst, int32_t* labels,
                      QEntry* queue, uint32_t* qcount, uint2* chg, uint32_t* chg_cnt, int delta, int n_cu,
-                     QLayout* ql, const int* gate, hipStream_t s) {
+                     QLayout* ql, const int* gate, hipStream_t s, int rev) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
@@ -1109,7 +1116,9 @@ hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, cons
   (void)nt;
 #define KM_S1_CASE(NS2_, NB_)                                                                                   \
   case NS2_ * 100 + NB_:                                                                                        \
-    if (delta)                                                                                                  \
+    if (delta && rev && KM_S1_SERP && NS2_ == 2 && NB_ == 8)                                                    \
+      KM_TIMED_LAUNCH((k_s1<2, 8, 1, true>), dim3(nbk), dim3(S1_WAVES * 64), lds, s, a);                        \
+    else if (delta)                                                                                             \
       KM_TIMED_LAUNCH((k_s1<NS2_, NB_, 1>), dim3(nbk), dim3(S1_WAVES * 64), lds, s, a);                         \
     else                                                                                                        \
       KM_TIMED_LAUNCH((k_s1<NS2_, NB_, 0>), dim3(nbk), dim3(S1_WAVES * 64), lds, s, a);                         \

@@ -215,6 +215,17 @@ def test_fit_c3_shape_delta_iterations():
     assert last["q_full"] + last["q_rerank"] < 0.002 * len(X), last
 
 
+@pytest.mark.parametrize("iters", [4, 5])
+def test_fit_serpentine_delta_iterations_ragged(iters):
+    # the c3-class delta fit alternates its sweep (k_s1<2, 8, 1, true> maps the
+    # tiles last-first on every other launch where X is <= 8 GiB): even and odd
+    # iteration counts end on either direction; a ragged last tile (n % 16 = 7)
+    # is first in the descending sweep
+    X = _blobs(40_007, 64, 200, seed=21)
+    C0 = X[np.random.default_rng(5).choice(len(X), 256, replace=False)]
+    _check_fit(X, C0, iters)
+
+
 def test_fit_noise_delta_iterations():
     # randn: no cluster structure, many rows change clusters every iteration
     rng = np.random.RandomState(42)
