@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("KM_LIB") or os.path.join(HERE, "libkmeans_amd.so")
 ROOT = os.path.dirname(HERE)
 HEADER = os.path.join(ROOT, "include", "kmeans_amd.h")
 
-KM_ABI_VERSION = 5
+KM_ABI_VERSION = 6
 KM_OK = 0
 KM_EMPTY = 1
 
@@ -43,7 +43,8 @@ class KmStatus(ctypes.Structure):
 class KmInfo(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int64), ("d", ctypes.c_int32), ("dp", ctypes.c_int32), ("k", ctypes.c_int32),
                 ("kp", ctypes.c_int32), ("path", ctypes.c_int32), ("n_cu", ctypes.c_int32),
-                ("device", ctypes.c_int32), ("fused_stats", ctypes.c_int32)]
+                ("device", ctypes.c_int32), ("fused_stats", ctypes.c_int32),
+                ("delta_stats", ctypes.c_int32)]
 
 
 _P = ctypes.c_void_p

@@ -107,6 +107,7 @@ struct km_ctx {
   bool x3_stale = true;          // Chi/Clo/cn2s/bnd not made for the prepared centroids (ensure_x3)
   bool sweep_rev = false;        // the last k_assign_small / k_s1 launch swept the rows last-first
   int stats_pending = 0;         // the last assign left 0 nothing, 1 full sums, 2 deltas in stats
+  bool last_delta = false;       // the last assign with statistics left deltas (km_info.delta_stats)
   float* bal = nullptr;  // fast screen: image error maxima (2 floats)
   // statistics already zero (the batch update cleared them): no memset
   bool stats_clean = false;
@@ -482,7 +483,8 @@ bool one_screen(km_ctx* c) {
 bool use_s1(km_ctx* c, bool with_stats) {
   if (!c->s1) return false;
   if (c->screen_forced >= 0 && c->screen_forced != KM_SCREEN_S1) return false;
-  return !with_stats || (c->delta_ready && !c->want_sse && km::s1_delta_ok(c->g, c->n_cu));
+  // (a caller that took the buffer with km_stats_buffer reads full sums)
+  return !with_stats || (c->delta_ready && !c->want_sse && !c->stats_exported && km::s1_delta_ok(c->g, c->n_cu));
 }
 
 // before an update reads the statistics: delta -> fold into the full sums;
@@ -523,6 +525,14 @@ int run_assign(km_ctx* c, bool with_stats) {
     if (rc != KM_OK) return rc;
   }
   c->ql = km::QLayout{0, 0};
+  if (with_stats && c->stats_pending == 2) {
+    // a second km_assign_stats before the update: the first one's labels are
+    // in place but its deltas were never folded into stats_full, so the
+    // deltas against those labels would describe the wrong base; this pass
+    // computes full sums instead (the same choice on every rank: it depends
+    // on the call sequence only)
+    c->delta_ready = false;
+  }
   const bool sse = with_stats && c->want_sse;
   double* sse_slot = c->stats + (size_t)g.k * (g.d + 1);
   if (with_stats && !c->stats_clean) KM_HIP(hipMemsetAsync(c->stats, 0, sizeof(double) * stats_len(g), c->stream));
@@ -534,7 +544,12 @@ int run_assign(km_ctx* c, bool with_stats) {
     c->ql = km::QLayout{0, g.n > 0 ? 1u : 0u};  // its last workgroup leaves the queued rows in qcount[0]
     return KM_OK;
   }
-  c->stats_pending = with_stats ? 1 : 0;
+  // (a predict between an assign and its update leaves that assign's
+  // statistics pending: the update still folds them)
+  if (with_stats) {
+    c->stats_pending = 1;
+    c->last_delta = false;
+  }
   if (use_s1(c, with_stats)) {
     {
       ProfScope ps(c, KM_K_ASSIGN, true);
@@ -556,7 +571,10 @@ int run_assign(km_ctx* c, bool with_stats) {
       ProfScope ps(c, KM_K_STATS);
       KM_HIP(km::launch_s1_delta(c->X, g, c->chg, c->chg_cnt, c->stats, c->n_cu, c->gate, c->stream));
     }
-    c->stats_pending = with_stats ? 2 : 0;
+    if (with_stats) {
+      c->stats_pending = 2;
+      c->last_delta = true;
+    }
     return KM_OK;
   }
   if (c->fused) {
@@ -753,6 +771,7 @@ int km_info_get(km_ctx* c, km_info* out) {
   out->n_cu = c->n_cu;
   out->device = c->device;
   out->fused_stats = (c->path == 1) || c->fused;
+  out->delta_stats = c->last_delta ? 1 : 0;
   return KM_OK;
 }
 

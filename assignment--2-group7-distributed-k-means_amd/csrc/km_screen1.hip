@@ -1013,13 +1013,15 @@ size_t s1_chg_entries(const Geometry& g, int n_cu) {
 
 size_t s1_wave_slots(int n_cu) { return (size_t)n_cu * S1_WAVES; }
 
-// the delta aggregation's LDS table [k][d+1] f64 and the wave-count prefix fit
-bool s1_delta_ok(const Geometry& g, int n_cu) {
-  int nbk;
-  uint32_t seg;
-  const int64_t nw = s1_grid(g, n_cu, &nbk, &seg);
-  return (size_t)g.k * (g.d + 1) * 8 + (size_t)(nw + 1) * 4 <= 160 * 1024 && g.k <= 65535;
+// the delta aggregation's LDS table [k][d+1] f64 and the wave-count prefix
+// for the largest grid (n_cu workgroups): geometry and device only, never the
+// rank's row count, so every rank of a job makes the same choice (a rank with
+// few rows has a smaller grid; sizing by its own grid could put it in delta
+// mode while a larger rank sends full sums into the same all-reduce)
+static size_t s1_delta_lds(const Geometry& g, int n_cu) {
+  return (size_t)g.k * (g.d + 1) * 8 + (size_t)(s1_wave_slots(n_cu) + 1) * 4;
 }
+bool s1_delta_ok(const Geometry& g, int n_cu) { return s1_delta_lds(g, n_cu) <= 160 * 1024 && g.k <= 65535; }
 
 hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt,
                            double* stats, int n_cu, const int* gate, hipStream_t s) {
@@ -1027,8 +1029,8 @@ hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, 
   int nbk;
   uint32_t seg;
   const int64_t nw = s1_grid(g, n_cu, &nbk, &seg);
-  const size_t lds = (size_t)g.k * (g.d + 1) * 8 + (size_t)(nw + 1) * 4;
-  if (lds > 160 * 1024 || g.k > 65535) return hipErrorInvalidValue;
+  const size_t lds = s1_delta_lds(g, n_cu);  // (nw <= n_cu * S1_WAVES)
+  if (!s1_delta_ok(g, n_cu)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_s1_delta, dim3(n_cu), dim3(1024), lds, s, X, g.dp, g.d, g.k, chg, chg_cnt, (int)nw, seg, stats,
                      gate);
   return hipGetLastError();

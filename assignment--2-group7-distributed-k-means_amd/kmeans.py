@@ -43,6 +43,7 @@ class LloydRunner:
         self.last = None
         self.device_repairs = 0  # iterations whose empty clusters the device replaced
         self.iterations_ran = 0  # iterations the device ran in batches (bench.py divides by these)
+        self.host_ms = None      # {call kind: host wall ms} while a caller times run() (bench.py)
         # takeSample's Bernoulli pass on the GPU when the engine has one
         self.sampler = getattr(engine, "bernoulli", None)
 
@@ -93,6 +94,9 @@ class LloydRunner:
         that ran exactly as ``iteration`` does.  Returns True on convergence."""
         it = first
         eng = self.engine
+        # host wall time per call kind (bench.py's N > 1 lines): None = off
+        ht = self.host_ms
+        clk = time.perf_counter
         # the batch size carries over between calls on one runner (a caller
         # running the loop in pieces, like bench.py's warmup and timed region)
         size = getattr(self, "_next_batch", self.batch)
@@ -101,21 +105,33 @@ class LloydRunner:
             # the repair seed of each iteration, int(time.time()) read per
             # iteration as L196 reads it per repair
             seeds = [model._empty_seed() for _ in range(m)]
+            t = clk()
             if self.device_repair == 2:
                 eng.repair_bind()
                 if eng.repair_state()[0]:                      # armed: every rank needs the same seeds
                     seeds = self.comm.broadcast_obj(seeds)
             eng.batch_begin()
+            if ht is not None:
+                ht["batch_begin"] = ht.get("batch_begin", 0.0) + (clk() - t) * 1e3
             try:
                 for b in range(m):
+                    t0 = clk()
                     eng.assign_stats()                         # L272 (+ L169-171 map side)
+                    t1 = clk()
                     self.comm.allreduce_stats(eng)             # L169-173 shuffle + collect
+                    t2 = clk()
                     # L176-206 (+ the repair's seed, L196), device convergence test
                     eng.update_async(model.tolerance, seeds[b])
+                    t3 = clk()
                     if self.device_repair == 2 and eng.repair_state()[1]:
                         # the picked rows from their owners (L196-200), then the rest
                         # of the update on the device
                         eng.repair_exchange(self.comm.dist.all_reduce)
+                    if ht is not None:
+                        t4 = clk()
+                        for key, v in (("assign_stats", t1 - t0), ("allreduce", t2 - t1),
+                                       ("update_async", t3 - t2), ("repair", t4 - t3)):
+                            ht[key] = ht.get(key, 0.0) + v * 1e3
             except BaseException:
                 # close the batch (the gate comes down, the context is back to
                 # the last iteration that ran), then report the original error
@@ -124,7 +140,10 @@ class LloydRunner:
                 except Exception:
                     pass
                 raise
+            t = clk()
             recs = eng.batch_end(m)
+            if ht is not None:
+                ht["batch_end"] = ht.get("batch_end", 0.0) + (clk() - t) * 1e3
             self.iterations_ran += len(recs)
             # a batch that ran through doubles the next one (fewer host round
             # trips on long runs); a stopped one (convergence, empties) resets it
@@ -227,7 +246,12 @@ class LabelsRDD(LocalRDD):
       an empty array.  ``everywhere=True`` (per call, or for the object at
       construction) gives every rank the whole list (one all-gather);
     * ``count()`` sums the shard lengths;
-    * ``local()`` is this rank's shard with no communication."""
+    * ``local()`` is this rank's shard with no communication;
+    * the other RDD methods inherited from ``LocalRDD`` (``glom``,
+      ``mapPartitions``, ``partition_array`` ...) run without communication
+      on this rank's shard (one partition), or on every label once
+      ``collect(everywhere=True)`` gathered them; with one rank that is the
+      whole result."""
 
     def __init__(self, local_labels: np.ndarray, comm: Communicator, everywhere: bool = False):
         self._local = local_labels
@@ -236,6 +260,16 @@ class LabelsRDD(LocalRDD):
         self._all = None     # every rank's labels (everywhere)
         self._root = None    # the driver's copy (rank 0)
         super().__init__([])
+
+    @property
+    def _parts(self):
+        # what the inherited LocalRDD methods see (never a collective: an
+        # inherited method may run on one rank only)
+        return [self._all if self._all is not None else self._local]
+
+    @_parts.setter
+    def _parts(self, value):  # LocalRDD.__init__ assigns it; the labels are the data
+        pass
 
     def _gather(self, everywhere: Optional[bool]) -> np.ndarray:
         ev = self._everywhere if everywhere is None else everywhere

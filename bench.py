@@ -67,6 +67,7 @@ def parse():
                    help="after the fit steps, time P predict passes (km_predict, labels left in HBM; "
                         "kmeans_spark.py:321-352) and add a 'predict' object to the line")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work per worker")
+    p.add_argument("--no-first-iter", action="store_true", help="skip the first-iterations timing (first_iter)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="per-launch HBM bytes from a rocprofv3 --pmc pass (optional)")
     return p.parse_args()
@@ -131,15 +132,22 @@ def cpu_baseline(d, k, n_total, seconds):
     rate = cb.calibrate(d, k)
     per = int(max(2000, min(400_000, rate * seconds)))
     with get_context("spawn").Pool(workers) as pool:
-        t0 = time.perf_counter()
-        res = pool.starmap(cb.run_partition, [(d, k, per, w) for w in range(workers)])
-        dt = time.perf_counter() - t0
+        # the workers generate their partitions, then start their passes
+        # together; the rate is timed over the passes only (first start to
+        # last end on the shared monotonic clock), not over process spawn,
+        # imports or data generation
+        # (spawn + numpy import + a partition of <= 400k rows: a few seconds;
+        # a late worker starts at once and its lag counts against the rate)
+        start_at = time.monotonic() + 6.0 + per * d * 2e-8
+        res = pool.starmap(cb.run_partition, [(d, k, per, w, start_at) for w in range(workers)])
+    dt = max(r[2] for r in res) - min(r[1] for r in res)
     pts = sum(r[0] for r in res)
     pps = pts / dt
     return {"value": pps / n_total, "unit": f"Lloyd it/s (extrapolated to N={n_total:,})", "cores": workers,
             "kind": "port", "points_per_sec": pps, "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
             "sample": f"{workers} workers x {per} points, d={d}, k={k}, one assign+combine pass each "
-                      f"(oracle/cpu_baseline.py restating kmeans_spark.py:147-173); it/s = points/s / N"}
+                      f"(oracle/cpu_baseline.py restating kmeans_spark.py:147-173), passes started together and "
+                      f"timed first start to last end (no spawn/import/data generation); it/s = points/s / N"}
 
 
 def main():
@@ -181,12 +189,15 @@ def main():
     # launch's ~6 us of stream time would be 4% of the step)
     eng.profile(True, phases=("assign", "stats"), every=4 if args.config in ("c1", "c2") else 1)
     ran0 = run.iterations_ran
+    if world > 1:
+        run.host_ms = {}   # host wall time per call kind (LloydRunner.run): where a multi-rank step goes
     t0 = time.perf_counter()
     run.run(km, log, args.warmup + args.steps, first=args.warmup)
     eng.sync()
     torch.cuda.synchronize()
     comm.barrier()
     t1 = time.perf_counter()
+    host_ms, run.host_ms = run.host_ms, None
     # iterations the device actually ran in the timed region: a batch stops
     # early only on convergence (max_shift < 1e-300, i.e. an exact fixed
     # point), empties or NaN; the rate counts what ran, never args.steps
@@ -337,6 +348,25 @@ def main():
                 "note": "ms_per_pass: host wall time per km_predict (launch + sync, labels left in HBM); "
                         "gb_s: rows read once (N*d*4) / HIP-event time of the assign launch"}
 
+    # the iterations after new centroids (kmeans_spark.py:266-318 from the
+    # start of a fit): the first runs the full-statistics screen (and, on the
+    # k_s1 geometries, colours the chains), the second is the first delta
+    # pass; steady state (ms_per_step) excludes both.  Host wall time of each
+    # with its own sync, after the same set_centroids a fit makes
+    first_iter = None
+    if not args.no_first_iter:
+        eng.set_centroids(C0)
+        first_iter = {}
+        for i in range(2):
+            comm.barrier()
+            tf0 = time.perf_counter()
+            run.run(km, log, i + 1, first=i)
+            eng.sync()
+            tf1 = time.perf_counter()
+            first_iter[f"iter{i + 1}_ms"] = (tf1 - tf0) * 1e3
+        first_iter["note"] = ("host wall time per iteration with a sync, after set_centroids(C0): iter1 = full "
+                              "statistics pass (first screen after new centroids), iter2 = the first pass of the "
+                              "steady-state path (k_s1 with delta statistics on the c3 class)")
     if rank == 0:
         it_s = ran / dt
         out = {
@@ -352,6 +382,8 @@ def main():
             "resolve": {"q_rerank": run.last["q_rerank"], "q_full": run.last["q_full"]} if run.last else None,
             "empty_repairs_on_device": run.device_repairs,
             "screen": screen,
+            "first_iter": first_iter,
+            "host_ms_per_step": ({kk: v / max(ran, 1) for kk, v in host_ms.items()} if host_ms else None),
             "predict": pred,
             "arith": ("fp16 MFMA screen (balanced image, pairwise bound)" if screen in (2, 3) else
                       "one fp16 MFMA per product, candidates re-scored in fp32 with a rigorous bound" +

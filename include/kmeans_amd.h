@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KM_ABI_VERSION 5
+#define KM_ABI_VERSION 6
 
 #define KM_OK 0
 #define KM_EMPTY 1          /* informational: the update found empty clusters */
@@ -75,6 +75,9 @@ typedef struct km_info {
   int32_t n_cu;      /* compute units of the device                   */
   int32_t device;
   int32_t fused_stats;
+  int32_t delta_stats; /* ABI 6: the last km_assign_stats left changes since the
+                          previous assignment in the stats buffer (delta
+                          statistics, see km_assign_stats), not full sums */
 } km_info;
 
 /* Kernel kinds for km_prof_read. */
@@ -126,12 +129,26 @@ int km_get_centroids(km_ctx* ctx, int32_t which, double* out);
  * rdd.mapPartitions(assign_partition) + the map-side combine of
  * reduceByKey (kmeans_spark.py:147-171).  Output = the stats buffer
  * (float64 [k][d+1]: per-cluster sum of x, then count; then one SSE slot,
- * 0 unless km_set_sse is on). */
+ * 0 unless km_set_sse is on).
+ * Delta statistics (ABI 5, the k_s1 screen's geometries, compute_sse off):
+ * from the second iteration after new centroids / rows / a predict, the
+ * buffer holds only the CHANGES since the previous assignment (rows that
+ * moved: -x, -1 on the old cluster, +x, +1 on the new one), and the context
+ * keeps the full sums itself; the update folds the (all-reduced) changes
+ * into them.  Summing the buffer over ranks is valid either way (every rank
+ * takes the same path: the choice depends on the call sequence and the
+ * geometry only).  After a batch update the buffer is zero.  A caller that
+ * reads the sums themselves takes the buffer with km_stats_buffer, which
+ * turns delta statistics off for the context (full sums every iteration). */
 int km_assign_stats(km_ctx* ctx);
 /* The stats buffer (device) and its length in doubles, k (d+1) + 1; a caller
  * may bind an external device buffer instead (e.g. a torch tensor it
  * all-reduces): this is the reduceByKey shuffle + collect
- * (kmeans_spark.py:169-173) and the partition-SSE .sum() (:237). */
+ * (kmeans_spark.py:169-173) and the partition-SSE .sum() (:237).
+ * km_stats_buffer: the buffer then always holds full sums after
+ * km_assign_stats (delta statistics off).  km_bind_stats_buffer keeps delta
+ * statistics on: the bound buffer carries the sums or the changes as
+ * described at km_assign_stats, which is what a sum all-reduce needs. */
 int km_stats_buffer(km_ctx* ctx, void** dev_ptr, int64_t* len);
 int km_bind_stats_buffer(km_ctx* ctx, void* dev_ptr);
 

@@ -54,9 +54,17 @@ def calibrate(d, k, n=2000):
     return n / (time.perf_counter() - t0)
 
 
-def run_partition(d, k, n, seed):
+def run_partition(d, k, n, seed, start_at=None):
+    """One partition's pass; returns (points, pass start, pass end) on the
+    system-wide monotonic clock (time.monotonic, shared by the worker
+    processes), so the caller times only the passes, not the workers'
+    start-up, imports or data generation.  ``start_at``: wait until that
+    monotonic time, so every worker's pass starts together."""
     X, C = _sample(d, k, n, seed + 1)
     rows = _cached_rows(X)
-    t0 = time.perf_counter()
+    if start_at is not None:
+        while time.monotonic() < start_at:
+            time.sleep(min(0.01, max(0.0, start_at - time.monotonic())))
+    t0 = time.monotonic()
     _partition_pass(rows, C)
-    return n, time.perf_counter() - t0
+    return n, t0, time.monotonic()

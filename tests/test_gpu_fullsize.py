@@ -152,3 +152,43 @@ def test_full_size_c2_through_lloyd_runner():
     # sums over the counts (checked above); predict with them is stable
     pred = eng.predict()
     np.testing.assert_array_equal(pred[gidx], orc.assign(Xs, C3)[0])
+
+
+def test_full_size_c3_delta_fit_through_lloyd_runner():
+    # the kernel the bench times (BASELINE metric, c3 = 100M x 64, k 256,
+    # compute_sse off): k_s1<2, 8, 1> with delta statistics (k_s1_delta, then
+    # k_s1_apply folding the changes into the kept full sums) at full size,
+    # through LloydRunner.run as fit drives it (kmeans_spark.py:147-206).
+    # Iterations 1-5 (the first with full statistics, then four delta passes),
+    # then iteration 6 alone so its input centroids are known: the counts are
+    # the label histogram, sum_j n_j c_j equals an independent float64 sum of X
+    # (the full sums after five rounds of deltas), and 20k sampled labels are
+    # the oracle's
+    import kmeans_amd
+    from kmeans_amd.comm import Communicator
+
+    N, d, k = 100_000_000, 64, 256
+    km = kmeans_amd.KMeans(k=k, max_iter=10, tolerance=1e-300, seed=42)
+    km.verbose = False
+    data = kmeans_amd.DeviceBlobs(n=N, d=d, n_centers=k, box=10.0, std=1.0, seed=2024)
+    run = km._make_runner(data, Communicator())
+    eng = run.engine
+    eng.set_centroids(km._initialize_centroids(run))
+    sx = eng.sum_x()
+    run.run(km, None, 5)
+    assert run.iterations_ran == 5
+    assert eng.screen() == 4 and eng.info()["delta_stats"] == 1
+    C_prev = eng.get_centroids(0)
+    run.run(km, None, 6, first=5)
+    assert run.iterations_ran == 6 and eng.info()["delta_stats"] == 1
+    counts = np.asarray(run.last["counts"])
+    C6 = eng.get_centroids(0)
+    labels = eng.labels()
+    assert int(counts.sum()) == N
+    np.testing.assert_array_equal(np.bincount(labels, minlength=k), counts)
+    nz = counts > 0
+    tot = (counts[nz, None].astype(np.float64) * C6[nz]).sum(axis=0)
+    np.testing.assert_allclose(tot, sx, rtol=1e-9, atol=1e-3)
+    gidx = np.sort(np.random.default_rng(13).choice(N, 20000, replace=False))
+    Xs = np.asarray(run.rows(gidx.tolist()), dtype=np.float64)
+    np.testing.assert_array_equal(labels[gidx], orc.assign(Xs, C_prev, chunk=1024)[0])

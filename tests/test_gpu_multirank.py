@@ -164,3 +164,75 @@ def test_two_ranks_delta_statistics_c3_shape():
         assert screen == 4, "k_s1 (delta statistics) not selected"
         np.testing.assert_allclose(C, ref["centroids"], rtol=1e-9, atol=1e-9)
         assert int(counts.sum()) == len(X)
+
+
+def _rank_uneven(rank, world, port, d, k, q):
+    # rank 0 holds all rows but 500, rank 1 the last 500: their k_s1 grids
+    # differ (rank 1 fills a few workgroups), and both must still make the
+    # same delta / full choice, or the all-reduce would add one rank's deltas
+    # to the other's full sums
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import kmeans_amd as ka
+        from kmeans_amd import dataset
+        X, C0 = _uneven_data(d, k)
+        dataset.rank_rows = lambda n, w, r: (0, n - 500) if r == 0 else (n - 500, n)
+
+        class Pinned(ka.KMeans):
+            def _initialize_centroids(self, run):
+                return C0.copy()
+
+            def _empty_seed(self):
+                return 1234
+
+        km = Pinned(k=k, max_iter=5, tolerance=1e-12, compute_sse=False)
+        km.verbose = False
+        km.fit(X)
+        eng = km._runner.engine
+        q.put((rank, km.centroids, eng.info()["delta_stats"], km._runner.pl.n_local, km._runner.last["counts"].copy()))
+    except Exception as e:  # surface the failure in the parent
+        q.put((rank, repr(e), None, None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _uneven_data(d, k):
+    rng = np.random.default_rng(95 + d)
+    C = rng.uniform(-10, 10, (300, d))
+    X = (C[rng.integers(0, 300, 20000)] + rng.standard_normal((20000, d))).astype(np.float32).astype(np.float64)
+    C0 = X[np.random.default_rng(96).choice(len(X), k, replace=False)]
+    return X, C0
+
+
+@pytest.mark.parametrize("d,k,delta", [
+    (18, 1000, 1),   # dp 32, kp 1024: the delta table fits for any grid -> deltas on both ranks
+    (19, 1000, 0),   # fits only beside a small grid's wave prefix -> full sums on both ranks
+])
+def test_two_ranks_uneven_shards_same_statistics_mode(d, k, delta):
+    import torch.multiprocessing as mp
+    from oracle import kmeans_oracle as orc
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_uneven, args=(r, 2, port, d, k, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=110) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0, res
+    X, C0 = _uneven_data(d, k)
+    assert [r[3] for r in res] == [len(X) - 500, 500]
+    ref = orc.lloyd_fit(X, k, 5, 1e-12, 0, False, 1, init_centroids=C0, empty_seed=lambda: 1234)
+    for rank, C, dstat, _, counts in res:
+        assert dstat == delta, (rank, dstat)
+        np.testing.assert_allclose(C, ref["centroids"], rtol=1e-9, atol=1e-9)
+        assert int(counts.sum()) == len(X)

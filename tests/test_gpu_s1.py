@@ -283,6 +283,126 @@ def test_fit_then_predict_then_fit_again():
     np.testing.assert_allclose(run.engine.get_centroids(0), ref["centroids"], rtol=1e-9, atol=1e-9)
 
 
+def test_long_delta_fit_no_drift_vs_full_statistics():
+    # the bench's steady state is a long run of delta iterations (the reference
+    # default is max_iter = 100, kmeans_spark.py:37): the full sums under the
+    # deltas are carried across every iteration of the fit, never re-based.
+    # 100 iterations on unstructured data at the c3 geometry (rows keep moving
+    # between clusters, tolerance 1e-300 never converges): identical labels and
+    # counts to the fit that recomputes full statistics every iteration
+    # (mode 1), centroids within float64 summation order of it, and the final
+    # centroids equal the float64 means of the rows under the final labels
+    # (np.add.at in the oracle's dtype), to 1e-9
+    rng = np.random.RandomState(7)
+    X = rng.randn(200_000, 64).astype(np.float32).astype(np.float64)
+    C0 = X[np.random.default_rng(8).choice(len(X), 256, replace=False)]
+    iters = 100
+    ka = _km()
+
+    def fit(mode):
+        from kmeans_amd.engine import make_engine
+
+        def factory(comm):
+            eng = make_engine(comm)
+            eng.set_screen(mode)
+            return eng
+
+        class Forced(ka.KMeans):
+            _engine_factory = staticmethod(factory)
+
+            def _initialize_centroids(self, run):
+                return C0.copy()
+
+            def _empty_seed(self):
+                return SEED
+
+        km = Forced(k=256, max_iter=iters, tolerance=1e-300, compute_sse=False)
+        km.verbose = False
+        km.fit(X)
+        return km
+
+    a, b = fit(-1), fit(1)
+    ea, eb = a._runner.engine, b._runner.engine
+    assert a._runner.iterations_ran == iters == b._runner.iterations_ran
+    assert ea.screen() == S1 and ea.info()["delta_stats"] == 1
+    assert eb.info()["delta_stats"] == 0
+    la = ea.labels()
+    np.testing.assert_array_equal(la, eb.labels())
+    np.testing.assert_array_equal(a._runner.last["counts"], b._runner.last["counts"])
+    np.testing.assert_allclose(a.centroids, b.centroids, rtol=1e-12, atol=1e-12)
+    counts = np.bincount(la, minlength=256)
+    np.testing.assert_array_equal(a._runner.last["counts"], counts)
+    sums = np.zeros((256, 64))
+    np.add.at(sums, la, X)
+    nz = counts > 0
+    np.testing.assert_allclose(a.centroids[nz], sums[nz] / counts[nz, None], rtol=1e-9, atol=1e-9)
+    # the last assignment against the oracle (the centroids it read are the
+    # ones before the last update: run one more oracle-free check on labels)
+    C_prev = ea.get_centroids(0)      # after the last update = the next pass's input
+    np.testing.assert_array_equal(ea.predict(), orc.assign(X, C_prev)[0])
+
+
+@pytest.mark.parametrize("n,d,k,centers,delta", [
+    (20000, 18, 1000, 300, True),    # dp 32, kp 1024 (unfused): k (d+1) 8 + the wave prefix fits LDS
+    (20000, 19, 1000, 300, False),   # dp 32, kp 1024: 160,000 B of table + the prefix do not fit
+    (20000, 97, 193, 100, True),     # dp 128, kp 256 (unfused)
+    (20000, 100, 200, 100, False),   # dp 128, kp 256: the table does not fit -> full statistics
+])
+def test_unfused_geometries_delta_statistics(n, d, k, centers, delta):
+    # the unfused k_s1 geometries take delta statistics where the [k][d+1]
+    # table and the largest grid's wave prefix fit LDS (km_screen1.hip
+    # s1_delta_ok: geometry and device only); their changed rows are resolved
+    # by the direct-atomic k_rerank2 / k_fullscan paths
+    X = _blobs(n, d, centers, seed=21 + k + d)
+    C0 = X[np.random.default_rng(22).choice(n, k, replace=False)]
+    km = _check_fit(X, C0, 5)
+    info = km._runner.engine.info()
+    assert info["fused_stats"] == 0
+    assert info["delta_stats"] == (1 if delta else 0)
+
+
+def test_assign_stats_twice_before_update():
+    # a caller that runs km_assign_stats twice before km_update:
+    # the first call's deltas were never folded, so the second computes full
+    # sums; the update then matches the oracle's one step, and later delta
+    # iterations stay exact
+    X = _blobs(30000, 64, 256, seed=91)
+    C0 = X[np.random.default_rng(92).choice(len(X), 256, replace=False)]
+    km = _fit(X, C0, 3)
+    run, eng = km._runner, km._runner.engine
+    C3 = eng.get_centroids(0)
+    eng.assign_stats()
+    assert eng.info()["delta_stats"] == 1
+    eng.assign_stats()
+    assert eng.info()["delta_stats"] == 0
+    st, counts = eng.update()
+    ref = orc.lloyd_fit(X, 256, 1, 1e-12, 0, False, 1, init_centroids=C3, empty_seed=lambda: SEED)
+    np.testing.assert_allclose(eng.get_centroids(1), ref["centroids"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_array_equal(counts, np.bincount(orc.assign(X, C3)[0], minlength=256))
+    eng.commit()
+    km.max_iter = 6
+    run.run(km, None, 6, first=4)
+    assert eng.info()["delta_stats"] == 1
+    ref2 = orc.lloyd_fit(X, 256, 2, 1e-12, 0, False, 1, init_centroids=ref["centroids"], empty_seed=lambda: SEED)
+    np.testing.assert_allclose(eng.get_centroids(0), ref2["centroids"], rtol=1e-9, atol=1e-9)
+
+
+def test_predict_between_assign_and_update_keeps_the_deltas():
+    # predict after a delta km_assign_stats and before its update: the update
+    # still folds that assignment's deltas (same centroids, same labels)
+    X = _blobs(30000, 64, 256, seed=93)
+    C0 = X[np.random.default_rng(94).choice(len(X), 256, replace=False)]
+    km = _fit(X, C0, 3)
+    eng = km._runner.engine
+    C3 = eng.get_centroids(0)
+    eng.assign_stats()
+    assert eng.info()["delta_stats"] == 1
+    np.testing.assert_array_equal(eng.predict(), orc.assign(X, C3)[0])
+    st, counts = eng.update()
+    ref = orc.lloyd_fit(X, 256, 1, 1e-12, 0, False, 1, init_centroids=C3, empty_seed=lambda: SEED)
+    np.testing.assert_allclose(eng.get_centroids(1), ref["centroids"], rtol=1e-9, atol=1e-9)
+
+
 def test_compute_sse_keeps_full_statistics():
     X = _blobs(20000, 64, 256, seed=51)
     C0 = X[np.random.default_rng(52).choice(len(X), 256, replace=False)]

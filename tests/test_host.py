@@ -34,7 +34,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert declared == set(_lib.exported_symbols()), declared ^ set(_lib.exported_symbols())
-    assert lib.km_abi_version() == 5
+    assert lib.km_abi_version() == 6
 
 
 def test_product_library_has_no_diagnostic_kernels():
