@@ -61,19 +61,31 @@ namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
 constexpr float U24 = 5.9604644775390625e-08f;  // 2^-24
 constexpr float U16 = 4.8828125e-04f;           // 2^-11, fp16 unit roundoff
-constexpr int S1_WAVES = 8;                     // 512 threads: two waves per SIMD
 constexpr int S1_LMAX = 8;                      // candidates re-scored per row
 #ifndef KM_S1_NBUF
 #define KM_S1_NBUF 0  // register buffers of rows (tiles in flight + 1); 0: by row length
 #endif
 #ifndef KM_S1_ABL
-#define KM_S1_ABL 0   // timing ablations (wrong labels): never in the product library
+#define KM_S1_ABL 0  // timing ablations (wrong labels): alt builds for A/B only, never the product
 #endif
 constexpr int ceil_log2_c(int v) { return v <= 1 ? 0 : 1 + ceil_log2_c((v + 1) / 2); }
-constexpr int S1_RING = 16;                     // rows per re-scoring batch (one per quad of a wave)
+// waves per workgroup (one workgroup per CU): three per SIMD on the c3
+// geometry (dp 64, kp 256), whose kernel is latency-bound at two (DESIGN.md
+// section 4), two elsewhere; KM_S1_W12=0 keeps two everywhere (A/B arm)
+#ifndef KM_S1_W12
+#define KM_S1_W12 1
+#endif
+constexpr int s1_waves(int ns2, int nb) { return (KM_S1_W12 && ns2 == 2 && nb == 8) ? 12 : 8; }
+
+constexpr int S1_MAX_WAVES = 12;                // per CU, any geometry (change-list counts)
+// rows per re-scoring batch (one per quad of a wave): 16, or 12 where twelve
+// waves' rings must fit beside the image and the fp32 table
+constexpr int s1_ring(int ns2, int nb) { return s1_waves(ns2, nb) == 12 ? 12 : 16; }
 
 // the re-scoring batches run where a wave's ring (S1_RING rows of DP floats,
 // 16 B of row data and 128 B of chain heads) fits beside the tables: dp <= 64
@@ -86,9 +98,6 @@ constexpr bool s1_batched(int ns2) { return ns2 <= 2; }
 #ifndef KM_S1_TT
 #define KM_S1_TT 1
 #endif
-#ifndef KM_S1_QUAD
-#define KM_S1_QUAD 0  // A/B knob: key updates four members at a time
-#endif
 constexpr int s1_tiles(int ns2) { return ns2 == 1 ? KM_S1_TT : 1; }
 
 // k_s1's LDS: image, fp32 table (unless it goes to global), norms, slots,
@@ -97,7 +106,7 @@ constexpr int s1_tiles(int ns2) { return ns2 == 1 ? KM_S1_TT : 1; }
 constexpr size_t s1_lds_bytes(int ns2, int nb, bool table) {
   const int dp = 32 * ns2, kp = 32 * nb, nt = 32 << ceil_log2_c(nb);
   return (size_t)kp * dp * 2 + (table ? (size_t)nt * (dp + 4) * 4 : 0) + (size_t)kp * 4 + (size_t)nt * 4 +
-         (s1_batched(ns2) ? (size_t)S1_WAVES * S1_RING * (dp * 4 + 16 + 128) : 0);
+         (s1_batched(ns2) ? (size_t)s1_waves(ns2, nb) * s1_ring(ns2, nb) * (dp * 4 + 16 + 128) : 0);
 }
 constexpr bool s1_table_global(int ns2, int nb) { return s1_lds_bytes(ns2, nb, true) > 160 * 1024; }
 
@@ -105,12 +114,29 @@ constexpr bool s1_table_global(int ns2, int nb) { return s1_lds_bytes(ns2, nb, t
 __device__ __forceinline__ uint32_t f2u(float v) { return __float_as_uint(v); }
 __device__ __forceinline__ float u2f(uint32_t v) { return __uint_as_float(v); }
 
+// minima of keys and heads without the IEEE-mode canonicalisation hipcc puts
+// in front of fminf for values made by bit operations (packed keys, lane
+// swaps, selects): every such value is finite here or its row is caught as
+// non-finite by the certificate (`bad`: the row-norm bound is NaN / inf), and
+// v_min / v_min3 order finite values exactly.  VALU results feeding VALU
+// only (never an MFMA operand: DESIGN.md section 2, inline asm and MFMA)
+__device__ __forceinline__ float min_raw(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float min3_raw(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // the four quarter lanes of a row (l, l ^ 16, l ^ 32, l ^ 48): min / sum
 __device__ __forceinline__ float quad_min(float v) {
   auto p = __builtin_amdgcn_permlane16_swap(f2u(v), f2u(v), false, false);
-  v = __builtin_fminf(u2f(p[0]), u2f(p[1]));
+  v = min_raw(u2f(p[0]), u2f(p[1]));
   p = __builtin_amdgcn_permlane32_swap(f2u(v), f2u(v), false, false);
-  return __builtin_fminf(u2f(p[0]), u2f(p[1]));
+  return min_raw(u2f(p[0]), u2f(p[1]));
 }
 // the same order of additions in all four lanes ((l0 + l16) + (l32 + l48)):
 // every lane of the row holds the bit-identical sum
@@ -310,8 +336,10 @@ struct S1Args {
 // read; only changed labels are written and moved in the sums; queued rows
 // keep their previous label for the resolvers to compare).
 template <int NS2, int NB, int MODE, bool REV = false>
-__global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
+__global__ __launch_bounds__(s1_waves(NS2, NB) * 64, s1_waves(NS2, NB) / 4) void k_s1(S1Args A) {
   if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
+  constexpr int S1_WAVES = s1_waves(NS2, NB);
+  constexpr int S1_RING = s1_ring(NS2, NB);
   constexpr int DP = 32 * NS2;
   constexpr int FQ = 8 * NS2;  // features per quarter lane
   constexpr int KP = 32 * NB;
@@ -401,18 +429,20 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     auto partial = [&](uint32_t slot) {
       const float4* cp = TG ? reinterpret_cast<const float4*>(A.cft + slot * CS + FQ * q)
                             : reinterpret_cast<const float4*>(sCf + slot * CS + FQ * q);
-      float acc = 0.0f;
+      // two packed chains (v_pk_add_f32 / v_pk_fma_f32 on feature pairs):
+      // each square and difference rounded once, FQ / 2 + 1 roundings per
+      // chain -- inside the re-score bound's (FQ + 4) u
+      f32x2 acc = {0.0f, 0.0f};
 #pragma unroll
       for (int u = 0; u < FQ / 4; ++u) {
         const float4 c = cp[u];
         const float4 x = xv[u];
-        const float d0 = x.x - c.x, d1 = x.y - c.y, d2 = x.z - c.z, d3 = x.w - c.w;
-        acc = fmaf(d0, d0, acc);
-        acc = fmaf(d1, d1, acc);
-        acc = fmaf(d2, d2, acc);
-        acc = fmaf(d3, d3, acc);
+        const f32x2 d0 = f32x2{x.x, x.y} - f32x2{c.x, c.y};
+        const f32x2 d1 = f32x2{x.z, x.w} - f32x2{c.z, c.w};
+        acc = __builtin_elementwise_fma(d0, d0, acc);
+        acc = __builtin_elementwise_fma(d1, d1, acc);
       }
-      return acc;
+      return acc.x + acc.y;
     };
     // winner (smallest upper bound U1, its lower bound L1, slot s1) and the
     // smallest lower bound of the others (Lo, slot s2), select form
@@ -534,7 +564,7 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
           if (__ballot(act && (uint32_t)r < cnt) == 0ull) break;
           float nl = FLT_MAX;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) nl = __builtin_fminf(nl, hv[i] > prev ? hv[i] : FLT_MAX);
+          for (int i = 0; i < 8; ++i) nl = min_raw(nl, hv[i] > prev ? hv[i] : FLT_MAX);
           prev = quad_min(nl);
           sl[r] = (uint32_t)r < cnt ? (f2u(prev) & SLOTM) : 0u;
         }
@@ -550,7 +580,7 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
 
   // everything after the chains of one tile: certificate, labels, queue,
   // re-scoring ring
-  auto tail = [&](uint32_t tile, const Buf& B, const float (&h)[2][4], const float (&h2)[2][4]) {
+  auto tail = [&](uint32_t tile, const Buf& B, const float (&h)[2][4], float h2m) {
     const uint32_t row = tmap(tile) * 16u + (uint32_t)c16;
     const bool valid = row < n;
     // full slot ids in the heads, (chain << MB) | member: distinct keys, so
@@ -561,10 +591,7 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) hk[cb][i] = u2f(f2u(h[cb][i]) | qbits | ((uint32_t)(16 * cb + i) << MB));
-    // the smallest second key of the lane's chains (an open chain: h2 <= T)
-    const float h2m = __builtin_fminf(
-        __builtin_fminf(__builtin_fminf(h2[0][0], h2[0][1]), __builtin_fminf(h2[0][2], h2[0][3])),
-        __builtin_fminf(__builtin_fminf(h2[1][0], h2[1][1]), __builtin_fminf(h2[1][2], h2[1][3])));
+    // h2m: the smallest second key of the lane's chains (an open chain: <= T)
 
     // the row's smallest head m, then the candidate threshold T (the
     // batched re-score finds the other candidates from the stored heads; the
@@ -575,9 +602,8 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     auto mx = [](float a, float b) { return __builtin_fmaxf(a, b); };
     float la = FLT_MAX, lb = FLT_MAX;
     if constexpr (BATCH) {
-      la = __builtin_fminf(
-          __builtin_fminf(__builtin_fminf(hk[0][0], hk[0][1]), __builtin_fminf(hk[0][2], hk[0][3])),
-          __builtin_fminf(__builtin_fminf(hk[1][0], hk[1][1]), __builtin_fminf(hk[1][2], hk[1][3])));
+      la = min3_raw(min3_raw(hk[0][0], hk[0][1], hk[0][2]), min3_raw(hk[0][3], hk[1][0], hk[1][1]),
+                    min3_raw(hk[1][2], hk[1][3], FLT_MAX));
       la = quad_min(la);
     } else {
 #pragma unroll
@@ -600,8 +626,8 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     }
     const float m = la;
 #if KM_S1_ABL == 1
-    // ablation (timing only, wrong labels): the screen core alone
-    if (valid && q == 0) A.labels[row] = sPerm[f2u(la) & SLOTM] + (h2[0][0] < -1e30f ? 1 : 0);
+    // timing ablation (diagnostic builds only, wrong labels): the screen core
+    if (valid && q == 0) A.labels[row] = sPerm[f2u(la) & SLOTM] + (h2m < -1e30f ? 1 : 0);
     return;
 #endif
     const float xn = B.xn;
@@ -636,7 +662,7 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     int32_t old = 0;
     if constexpr (MODE == 1) old = (int32_t)min((uint32_t)B.old, (uint32_t)(A.k - 1));
 #if KM_S1_ABL == 2
-    // ablation (timing only, wrong labels): no re-scoring
+    // timing ablation (diagnostic builds only, wrong labels): no re-scoring
     emit(valid, row, dec1 || needy ? 0u : 2u, labm, 0, old);
     return;
 #endif
@@ -684,7 +710,7 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) nl = __builtin_fminf(nl, hk[cb][i] > prev ? hk[cb][i] : FLT_MAX);
+          for (int i = 0; i < 4; ++i) nl = min_raw(nl, hk[cb][i] > prev ? hk[cb][i] : FLT_MAX);
         prev = quad_min(nl);
         sl[r] = f2u(prev) & SLOTM;
       }
@@ -705,29 +731,35 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
     for (int u = 0; u < TT; ++u)
 #pragma unroll
       for (int t = 0; t < NS2; ++t) {
+        // packed: four v_pk_mul_f32 and four v_cvt_pk_f16_f32 (round to
+        // nearest even) per eight features, halves in feature order
         const float4 a = BB[u].x[2 * t], c = BB[u].x[2 * t + 1];
-        bx[u][t][0] = (_Float16)(a.x * s);
-        bx[u][t][1] = (_Float16)(a.y * s);
-        bx[u][t][2] = (_Float16)(a.z * s);
-        bx[u][t][3] = (_Float16)(a.w * s);
-        bx[u][t][4] = (_Float16)(c.x * s);
-        bx[u][t][5] = (_Float16)(c.y * s);
-        bx[u][t][6] = (_Float16)(c.z * s);
-        bx[u][t][7] = (_Float16)(c.w * s);
+        const f32x2 sv = {s, s};
+        const f16x2 h0 = __builtin_convertvector(f32x2{a.x, a.y} * sv, f16x2);
+        const f16x2 h1 = __builtin_convertvector(f32x2{a.z, a.w} * sv, f16x2);
+        const f16x2 h2 = __builtin_convertvector(f32x2{c.x, c.y} * sv, f16x2);
+        const f16x2 h3 = __builtin_convertvector(f32x2{c.z, c.w} * sv, f16x2);
+        bx[u][t] = __builtin_shufflevector(__builtin_shufflevector(h0, h1, 0, 1, 2, 3),
+                                           __builtin_shufflevector(h2, h3, 0, 1, 2, 3), 0, 1, 2, 3, 4, 5, 6, 7);
       }
     // this lane's 8 chains per tile: best key (head, member id in the low MB
-    // bits) and second key
-    float h[TT][2][4], h2[TT][2][4];
+    // bits); and the smallest SECOND key over the lane's chains (h2m): the
+    // certificate only asks whether any chain's second key is under the
+    // threshold, i.e. min over chains of min over updates of
+    // med3(head, ka, kb), so one running minimum per tile replaces eight
+    // per-chain ones (fewer registers, half the minimum operations)
+    float h[TT][2][4], h2m[TT];
 #pragma unroll
-    for (int u = 0; u < TT; ++u)
+    for (int u = 0; u < TT; ++u) {
+      h2m[u] = FLT_MAX;
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) h[u][cb][i] = h2[u][cb][i] = FLT_MAX;
+        for (int i = 0; i < 4; ++i) h[u][cb][i] = FLT_MAX;
+    }
     const float4* cnl = reinterpret_cast<const float4*>(sCn + 4 * q);  // + 8 blk + 4 cb
     // a block pair's operands from LDS: A fragments (lane-linear 1 KiB
-    // pieces, conflict-free) and accumulator inits; the next pair's are
-    // read while this pair's MFMAs and key updates run
+    // pieces, conflict-free) and accumulator inits
     struct Pair {
       f16x8 a[2][2][NS2];  // [block of the pair][cb][t]
       float4 c[2][2];      // [block of the pair][cb]
@@ -743,12 +775,8 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
             P.a[e][cb][t] = __builtin_bit_cast(f16x8, sImg[(((blk + e) * 2 + cb) * NS2 + t) * 64 + lane]);
         }
     };
-    Pair pr[2];
-    load_pair(0, pr[0]);
-    // blocks in pairs: two members per step, new best = min3(best, ka, kb),
-    // new second = min(second, med3(best, ka, kb))
-    auto step = [&](int blk, const Pair& P) {
-      f32x4 a[TT][2][2];
+    // the MFMAs of a block pair (two members of every chain)
+    auto mfmas = [&](const Pair& P, f32x4 (&a)[TT][2][2]) {
 #pragma unroll
       for (int u = 0; u < TT; ++u)
 #pragma unroll
@@ -765,88 +793,101 @@ __global__ __launch_bounds__(S1_WAVES * 64, 2) void k_s1(S1Args A) {
 #pragma unroll
             for (int u = 0; u < TT; ++u)
               a[u][e][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(P.a[e][cb][t], bx[u][t], a[u][e][cb], 0, 0, 0);
+    };
+    // their keys: new head = min3(head, ka, kb), second-key minimum
+    // h2m = min(h2m, med3(head, ka, kb)) over the chains
+    auto keys = [&](int blk, const f32x4 (&a)[TT][2][2]) {
 #pragma unroll
-      for (int u = 0; u < TT; ++u)
+      for (int u = 0; u < TT; ++u) {
+        float t[2][4];
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const float ka = u2f((f2u(a[u][0][cb][i]) & KMASK) | (uint32_t)blk);
             const float kb = u2f((f2u(a[u][1][cb][i]) & KMASK) | (uint32_t)(blk + 1));
-            const float t = __builtin_amdgcn_fmed3f(h[u][cb][i], ka, kb);
+            t[cb][i] = __builtin_amdgcn_fmed3f(h[u][cb][i], ka, kb);
             h[u][cb][i] = __builtin_fminf(__builtin_fminf(h[u][cb][i], ka), kb);
-            h2[u][cb][i] = __builtin_fminf(h2[u][cb][i], t);
           }
+        // (a chain of v_min3: two values per operation)
+        float m = h2m[u];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          m = __builtin_fminf(__builtin_fminf(m, t[cb][0]), t[cb][1]);
+          m = __builtin_fminf(__builtin_fminf(m, t[cb][2]), t[cb][3]);
+        }
+        h2m[u] = m;
+      }
     };
-    // one block pair in flight (plus the next one's operands): the scheduler
-    // would otherwise hoist every pair's reads and MFMAs ahead of the key
-    // updates; the partner wave on the SIMD fills the MFMA pipe while this one
-    // updates its keys
-    if constexpr (KM_S1_QUAD && TT == 1 && NB <= 8 && NB % 4 == 0) {
-      // A/B knob: keys of four members at a time, 9 operations per four keys
-      // instead of 10 (two pairs' accumulators live together)
-      auto mfma_only = [&](const Pair& P, f32x4 (&a)[2][2]) {
+    // keep the key state computed where it is (the compiler would otherwise
+    // sink the second-key updates into the certificate's branch and hold
+    // every key of the tile alive until then)
+    auto pin = [&]() {
 #pragma unroll
-        for (int e = 0; e < 2; ++e)
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb) a[e][cb] = f32x4{P.c[e][cb].x, P.c[e][cb].y, P.c[e][cb].z, P.c[e][cb].w};
-#pragma unroll
-        for (int t = 0; t < NS2; ++t)
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-            for (int e = 0; e < 2; ++e)
-              a[e][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(P.a[e][cb][t], bx[0][t], a[e][cb], 0, 0, 0);
-      };
-#pragma unroll
-      for (int blk = 0; blk < NB; blk += 4) {
-        f32x4 a[2][2], b2[2][2];
-        load_pair(blk + 2, pr[1]);
-        mfma_only(pr[0], a);
-        __builtin_amdgcn_sched_barrier(0);
-        if (blk + 4 < NB) load_pair(blk + 4, pr[0]);
-        mfma_only(pr[1], b2);
+      for (int u = 0; u < TT; ++u) {
+        asm volatile("" : "+v"(h2m[u]));
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float ka = u2f((f2u(a[0][cb][i]) & KMASK) | (uint32_t)blk);
-            const float kb = u2f((f2u(a[1][cb][i]) & KMASK) | (uint32_t)(blk + 1));
-            const float kc = u2f((f2u(b2[0][cb][i]) & KMASK) | (uint32_t)(blk + 2));
-            const float kd = u2f((f2u(b2[1][cb][i]) & KMASK) | (uint32_t)(blk + 3));
-            float& hh = h[0][cb][i];
-            const float s1v = __builtin_amdgcn_fmed3f(hh, ka, kb);
-            const float m1 = __builtin_fminf(__builtin_fminf(hh, ka), kb);
-            const float s2v = __builtin_amdgcn_fmed3f(m1, kc, kd);
-            hh = __builtin_fminf(__builtin_fminf(m1, kc), kd);
-            h2[0][cb][i] = __builtin_fminf(__builtin_fminf(h2[0][cb][i], s1v), s2v);
-          }
+          for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(h[u][cb][i]));
+      }
+    };
+    if constexpr (NB <= 8 && s1_waves(NS2, NB) == 12) {
+      // three waves per SIMD (<= 168 registers): ONE pair of operands in
+      // registers -- the MFMAs of a pair read it, then it is refilled with
+      // the next pair's while this pair's keys are updated (round 6 A/B on
+      // one box, profiles/r6_c3_s1_waves_ab.json: 7.81-7.84 ms against
+      // 7.90-7.94 at two waves per SIMD with two operand sets, 7.89 with the
+      // MFMAs of pair p beside the keys of pair p - 1, 8.04-8.11 with the
+      // keys interleaved between the MFMAs by sched_group_barrier)
+      Pair P;
+      load_pair(0, P);
+#pragma unroll
+      for (int blk = 0; blk < NB; blk += 2) {
+        f32x4 a[TT][2][2];
+        mfmas(P, a);
+        __builtin_amdgcn_sched_barrier(0);
+        if (blk + 2 < NB) load_pair(blk + 2, P);
+        __builtin_amdgcn_sched_barrier(0);
+        keys(blk, a);
+        pin();
         __builtin_amdgcn_sched_barrier(0);
       }
     } else if constexpr (NB <= 8) {
+      // one block pair in flight plus the next one's operands: the partner
+      // wave on the SIMD fills the MFMA pipe while this one updates its keys
+      Pair pr[2];
+      load_pair(0, pr[0]);
 #pragma unroll
       for (int blk = 0; blk < NB; blk += 2) {
         const Pair& P = pr[(blk >> 1) & 1];
         if (blk + 2 < NB) load_pair(blk + 2, pr[((blk >> 1) + 1) & 1]);
-        step(blk, P);
+        f32x4 a[TT][2][2];
+        mfmas(P, a);
+        keys(blk, a);
         __builtin_amdgcn_sched_barrier(0);
       }
     } else {
       // many members (NB a multiple of 4): two pairs per trip of a loop, the
       // member id a run-time value
       static_assert(NB % 4 == 0, "NB > 8 must be a multiple of 4");
+      Pair pr[2];
+      load_pair(0, pr[0]);
 #pragma unroll 1
       for (int blk = 0; blk < NB; blk += 4) {
+        f32x4 a[TT][2][2];
         load_pair(blk + 2, pr[1]);
-        step(blk, pr[0]);
+        mfmas(pr[0], a);
+        keys(blk, a);
         __builtin_amdgcn_sched_barrier(0);
         if (blk + 4 < NB) load_pair(blk + 4, pr[0]);
-        step(blk + 2, pr[1]);
+        mfmas(pr[1], a);
+        keys(blk + 2, a);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
 #pragma unroll
-    for (int u = 0; u < TT; ++u) tail(st * TT + (uint32_t)u, BB[u], h[u], h2[u]);
+    for (int u = 0; u < TT; ++u) tail(st * TT + (uint32_t)u, BB[u], h[u], h2m[u]);
   };
 
   // this wave's steps gw, gw + nw, ... of TT tiles each; NBUF register
@@ -993,13 +1034,15 @@ __global__ __launch_bounds__(1024) void k_s1_delta(const float* __restrict__ X, 
 // ---------------------------------------------------------------------------
 // k_s1's grid: workgroups (one per CU at most, 8 waves each) and the rows
 // of one wave's queue / change-list segment
+static int s1_geo_waves(const Geometry& g) { return s1_waves(g.dp / 32, g.kp / 32); }
 static int64_t s1_grid(const Geometry& g, int n_cu, int* nbk, uint32_t* seg) {
   const int tt = s1_tiles(g.dp / 32);
+  const int w = s1_geo_waves(g);
   const int64_t nst = ((g.n + 15) / 16 + tt - 1) / tt;  // wave steps of tt tiles
   int64_t blocks = n_cu;
-  if (blocks > (nst + S1_WAVES - 1) / S1_WAVES) blocks = (nst + S1_WAVES - 1) / S1_WAVES;
+  if (blocks > (nst + w - 1) / w) blocks = (nst + w - 1) / w;
   *nbk = (int)blocks;
-  const int64_t nw = blocks * S1_WAVES;
+  const int64_t nw = blocks * w;
   *seg = nw ? (uint32_t)(((nst + nw - 1) / nw) * 16 * tt) : 0u;
   return nw;
 }
@@ -1011,7 +1054,7 @@ size_t s1_chg_entries(const Geometry& g, int n_cu) {
   return (size_t)std::max<int64_t>(nw * (int64_t)seg, 1);
 }
 
-size_t s1_wave_slots(int n_cu) { return (size_t)n_cu * S1_WAVES; }
+size_t s1_wave_slots(int n_cu) { return (size_t)n_cu * S1_MAX_WAVES; }
 
 // the delta aggregation's LDS table [k][d+1] f64 and the wave-count prefix
 // for the largest grid (n_cu workgroups): geometry and device only, never the
@@ -1019,7 +1062,7 @@ size_t s1_wave_slots(int n_cu) { return (size_t)n_cu * S1_WAVES; }
 // few rows has a smaller grid; sizing by its own grid could put it in delta
 // mode while a larger rank sends full sums into the same all-reduce)
 static size_t s1_delta_lds(const Geometry& g, int n_cu) {
-  return (size_t)g.k * (g.d + 1) * 8 + (size_t)(s1_wave_slots(n_cu) + 1) * 4;
+  return (size_t)g.k * (g.d + 1) * 8 + ((size_t)n_cu * s1_geo_waves(g) + 1) * 4;
 }
 bool s1_delta_ok(const Geometry& g, int n_cu) { return s1_delta_lds(g, n_cu) <= 160 * 1024 && g.k <= 65535; }
 
@@ -1029,7 +1072,7 @@ hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, 
   int nbk;
   uint32_t seg;
   const int64_t nw = s1_grid(g, n_cu, &nbk, &seg);
-  const size_t lds = s1_delta_lds(g, n_cu);  // (nw <= n_cu * S1_WAVES)
+  const size_t lds = s1_delta_lds(g, n_cu);  // (nw <= n_cu * waves)
   if (!s1_delta_ok(g, n_cu)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_s1_delta, dim3(n_cu), dim3(1024), lds, s, X, g.dp, g.d, g.k, chg, chg_cnt, (int)nw, seg, stats,
                      gate);
@@ -1119,11 +1162,11 @@ hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, cons
 #define KM_S1_CASE(NS2_, NB_)                                                                                   \
   case NS2_ * 100 + NB_:                                                                                        \
     if (delta && rev && KM_S1_SERP && NS2_ == 2 && NB_ == 8)                                                    \
-      KM_TIMED_LAUNCH((k_s1<2, 8, 1, true>), dim3(nbk), dim3(S1_WAVES * 64), lds, s, a);                        \
+      KM_TIMED_LAUNCH((k_s1<2, 8, 1, true>), dim3(nbk), dim3(s1_waves(2, 8) * 64), lds, s, a);                  \
     else if (delta)                                                                                             \
-      KM_TIMED_LAUNCH((k_s1<NS2_, NB_, 1>), dim3(nbk), dim3(S1_WAVES * 64), lds, s, a);                         \
+      KM_TIMED_LAUNCH((k_s1<NS2_, NB_, 1>), dim3(nbk), dim3(s1_waves(NS2_, NB_) * 64), lds, s, a);              \
     else                                                                                                        \
-      KM_TIMED_LAUNCH((k_s1<NS2_, NB_, 0>), dim3(nbk), dim3(S1_WAVES * 64), lds, s, a);                         \
+      KM_TIMED_LAUNCH((k_s1<NS2_, NB_, 0>), dim3(nbk), dim3(s1_waves(NS2_, NB_) * 64), lds, s, a);              \
     break;
   switch (sg.ns2 * 100 + sg.nb) {
     KM_S1_CASE(2, 2) KM_S1_CASE(2, 4) KM_S1_CASE(2, 6) KM_S1_CASE(2, 8)

@@ -1,4 +1,4 @@
-"""profiles/rN_c3_sq_counters.json from the SQ counter pass of scripts/gpu_final2.sh.
+"""profiles/rN_*_sq_*.json from an SQ counter pass of scripts/gpu_sq.sh.
 
 usage: python scripts/sq_summary.py gpurun_out/TAG OUT.json ["kernel name substring"] [config]
 Per dispatch of the kernel: duration from the pass's own timestamps, clock =
@@ -34,6 +34,10 @@ for disp in sorted(per):
                  "SQ_ACTIVE_INST_LDS", "SQ_BUSY_CYCLES"):
         if name in raw:
             row[name.lower()[3:]] = raw[name] / wc
+    # instruction counts per launch (SQ_INSTS_*)
+    for name in raw:
+        if name.startswith("SQ_INSTS_"):
+            row[name.lower()[3:] + "_per_launch"] = raw[name]
     if "SQ_LDS_IDX_ACTIVE" in raw:
         row["lds_active_per_cu_cycle"] = raw["SQ_LDS_IDX_ACTIVE"] / 256.0 / grbm
     if "SQ_LDS_BANK_CONFLICT" in raw and "SQ_LDS_IDX_ACTIVE" in raw:

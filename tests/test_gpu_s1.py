@@ -345,8 +345,7 @@ def test_long_delta_fit_no_drift_vs_full_statistics():
 @pytest.mark.parametrize("n,d,k,centers,delta", [
     (20000, 18, 1000, 300, True),    # dp 32, kp 1024 (unfused): k (d+1) 8 + the wave prefix fits LDS
     (20000, 19, 1000, 300, False),   # dp 32, kp 1024: 160,000 B of table + the prefix do not fit
-    (20000, 97, 193, 100, True),     # dp 128, kp 256 (unfused)
-    (20000, 100, 200, 100, False),   # dp 128, kp 256: the table does not fit -> full statistics
+    (20000, 60, 480, 200, False),    # dp 64, kp 512 (unfused): the table does not fit -> full statistics
 ])
 def test_unfused_geometries_delta_statistics(n, d, k, centers, delta):
     # the unfused k_s1 geometries take delta statistics where the [k][d+1]
