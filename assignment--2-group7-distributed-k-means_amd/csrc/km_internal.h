@@ -135,7 +135,8 @@ bool mfma_path_ok(const Geometry& g);
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
                           double* stats, int n_cu, const int* gate, hipStream_t s, double* sse = nullptr,
-                          const uint32_t* cand = nullptr, uint32_t cand_cap = 0, int delta = 0);
+                          const uint32_t* cand = nullptr, uint32_t cand_cap = 0, int delta = 0,
+                          const float* sse_c32 = nullptr);
 // Fused assign + partial sums (kp*dp <= 16384 class): fp16 hi image in VGPRs,
 // lo image + float64 sum table in LDS; decided points summed here, queued
 // points (and their counts) by launch_resolve(stats).
@@ -193,13 +194,15 @@ hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels
 // set); stop_tol >= 0 lets k_finalize raise it (KM_STOP_*), < 0 never
 // dev_repair: empty clusters are repaired on the device (launch_repair), so
 // they neither raise the gate nor allow a convergence stop here
+// corr: the SSE slot holds residuals to the fp32 images c' (k_s1 delta fit
+// with compute_sse); the update adds the exact per-cluster correction
 // clear / C32, cmax (one-workgroup update only, update_one_ok): zero the
 // statistics after use and write the small path's images of the new centroids
 bool update_one_ok(const Geometry& g);
 hipError_t launch_update(double* stats, const double* C64_old, const Geometry& g, double* C64_new,
                          double* work, int64_t* counts, const uint32_t* qcount, uint32_t nq, DevStatus* status,
                          int* gate, double stop_tol, int dev_repair, hipStream_t s, int clear = 0,
-                         float* C32 = nullptr, float* cmax = nullptr);
+                         float* C32 = nullptr, float* cmax = nullptr, int corr = 0);
 hipError_t launch_sum_x(const float* X, const Geometry& g, double* out, hipStream_t s);
 hipError_t launch_scatter_rows(const int64_t* ids, const double* rows, int32_t n, int d, double* C, hipStream_t s);
 hipError_t launch_gather_rows(const float* X, const Geometry& g, const int64_t* idx, int32_t n, double* out,
@@ -238,11 +241,12 @@ hipError_t launch_s1_prep(const double* C64, const float* C32, const Geometry& g
 hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, const uint4* img, const float* cn2o,
                      const float* cft, const int32_t* perm, const float* cst, int32_t* labels,
                      QEntry* queue, uint32_t* qcount, uint2* chg, uint32_t* chg_cnt, int delta, int n_cu,
-                     QLayout* ql, const int* gate, hipStream_t s, int rev = 0);
+                     QLayout* ql, const int* gate, hipStream_t s, int rev = 0, double* sse = nullptr);
 // k_s1's change list: entries (wave segments) and per-wave counts to allocate
 size_t s1_chg_entries(const Geometry& g, int n_cu);
 size_t s1_wave_slots(int n_cu);
-// delta statistics possible (k_s1_delta's table fits LDS)
+// delta statistics possible (16-bit cluster ids; k_s1_delta aggregates in
+// LDS where the [k][d+1] table fits, else with global float64 atomics)
 bool s1_delta_ok(const Geometry& g, int n_cu);
 // delta statistics: the change list of k_s1 into stats (deltas)
 hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt,

@@ -345,7 +345,7 @@ __device__ void update_one_body(double* __restrict__ stats, const double* __rest
                                 double* __restrict__ out, int64_t* __restrict__ counts, const double* __restrict__ sse,
                                 const uint32_t* __restrict__ qcount, uint32_t nq, DevStatus* __restrict__ st,
                                 int* __restrict__ gate, double stop_tol, int dev_repair, int clear,
-                                float* __restrict__ C32, float* __restrict__ cmax, int dp, int kp);
+                                float* __restrict__ C32, float* __restrict__ cmax, int dp, int kp, int corr = 0);
 
 // waves per SIMD at dp = 16 (KM_SMALL_WPE; c2 on one MI355X: 4 waves with the
 // row prefetch 146-147 us, 8 waves without it 154-161 us), the compiler's
@@ -3677,7 +3677,8 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
                                                   const uint32_t* __restrict__ qcount, QLayout ql,
                                                   int32_t* __restrict__ labels, double* __restrict__ stats,
                                                   int tab_kp, double* __restrict__ sse, const int* __restrict__ gate,
-                                                  const uint32_t* __restrict__ cand, uint32_t cand_cap, int delta) {
+                                                  const uint32_t* __restrict__ cand, uint32_t cand_cap, int delta,
+                                                  const float* __restrict__ sse_c32) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* tab = reinterpret_cast<double*>(smem);
@@ -3764,8 +3765,17 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
     const int old = delta ? (int)min((uint32_t)labels[q.row], (uint32_t)(k - 1)) : -1;
     if (u == 0) labels[q.row] = lab;
     // SSE (fused path): min_distance ** 2 with the chosen centroid's norm in
-    // NumPy's order (kmeans_spark.py:231-233)
-    if (sse && u == 0) {
+    // NumPy's order (kmeans_spark.py:231-233); with sse_c32 (k_s1's delta
+    // fit) the residual to the fp32 image c' of the centroid instead, as k_s1
+    // adds it for the rows it decides (the update corrects the total)
+    if (sse && sse_c32) {
+      double r = 0.0;
+      for (int f = u; f < d; f += 8) {
+        const double e = (double)x[f] - (double)sse_c32[(size_t)lab * dp + f];
+        r = fma(e, e, r);
+      }
+      ss_acc += r;
+    } else if (sse && u == 0) {
       const double mn = ok ? mnorm : rsq_bad;
       ss_acc += mn * mn;
     }
@@ -3850,7 +3860,8 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
                                                    const uint32_t* __restrict__ qcount, QLayout ql,
                                                    int32_t* __restrict__ labels, int ch,
                                                    double* __restrict__ stats, int use_chain, int pair_chain,
-                                                   double* __restrict__ sse, const int* __restrict__ gate, int delta) {
+                                                   double* __restrict__ sse, const int* __restrict__ gate, int delta,
+                                                   const float* __restrict__ sse_c32) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sCT = reinterpret_cast<double*>(smem);                                    // [d][ch]
@@ -3921,7 +3932,14 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
       // delta statistics (k_s1): the queued row still holds its previous label
       const int old = delta ? (int)min((uint32_t)labels[rows[g]], (uint32_t)(k - 1)) : -1;
       if (lane == 0) labels[rows[g]] = lab;
-      if (sse && lane == 0 && bi >= 0) ss_acc += bv * bv;  // min_distance ** 2 (bv: the norm)
+      if (sse && sse_c32) {  // k_s1's delta fit: the residual to c' (see k_rerank2)
+        for (int f = lane; f < d; f += 64) {
+          const double e = (double)xs[g * d + f] - (double)sse_c32[(size_t)lab * dp + f];
+          ss_acc = fma(e, e, ss_acc);
+        }
+      } else if (sse && lane == 0 && bi >= 0) {
+        ss_acc += bv * bv;  // min_distance ** 2 (bv: the norm)
+      }
       if (stats && delta) {
         if (old != lab) {  // the row moves from cluster old to lab
           for (int f = lane; f < d; f += 64) {
@@ -4068,13 +4086,16 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
     for (int g = 0; g < G; ++g)
       if (have[g]) finish(g, best[g], bj[g]);
   }
-  if (sse && lane == 0 && ss_acc != 0.0) atomicAdd(sse, ss_acc);
+  if (sse) {
+    ss_acc = wave_sum(ss_acc);  // (lane 0 alone, or every lane with sse_c32)
+    if (lane == 0 && ss_acc != 0.0) atomicAdd(sse, ss_acc);
+  }
 }
 
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
                           double* stats, int n_cu, const int* gate, hipStream_t s, double* sse,
-                          const uint32_t* cand, uint32_t cand_cap, int delta) {
+                          const uint32_t* cand, uint32_t cand_cap, int delta, const float* sse_c32) {
   if (g.n == 0 || ql.nwaves == 0) return hipSuccess;
   constexpr size_t LDS_MAX = 160 * 1024;
   const size_t pre_bytes = ((size_t)ql.nwaves + 1) * 4;
@@ -4095,15 +4116,15 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   if (ch == 0)
     hipLaunchKernelGGL((k_fullscan<2, true>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
                        queue, qcount, ql, labels, ch, delta ? stats : (double*)nullptr, use_chain, pair_chain, sse, gate,
-                       delta);
+                       delta, sse_c32);
   else if (G == 4)
     hipLaunchKernelGGL((k_fullscan<4, false>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
                        queue, qcount, ql, labels, ch, delta ? stats : (double*)nullptr, use_chain, pair_chain, sse, gate,
-                       delta);
+                       delta, sse_c32);
   else
     hipLaunchKernelGGL((k_fullscan<2, false>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
                        queue, qcount, ql, labels, ch, delta ? stats : (double*)nullptr, use_chain, pair_chain, sse, gate,
-                       delta);
+                       delta, sse_c32);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t tab_bytes = (size_t)(g.d + 1) * g.kp * 8;
@@ -4118,10 +4139,10 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   const int rwg = std::max(1, n_cu * std::max(1, rpct) / 100);
   if (g.d > 256)
     hipLaunchKernelGGL(k_rerank2<true>, dim3(rwg), dim3(512), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
-                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap, delta);
+                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap, delta, sse_c32);
   else
     hipLaunchKernelGGL(k_rerank2<false>, dim3(rwg), dim3(1024), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
-                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap, delta);
+                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap, delta, sse_c32);
   return hipGetLastError();
 }
 
@@ -4665,15 +4686,27 @@ hipError_t launch_stats_sorted(const float* X, const Geometry& g, const int32_t*
 // squared shift.  The SSE (L224-237) is the all-reduced residual slot
 // stats[k (d+1)] filled by the assign / statistics passes.
 // ---------------------------------------------------------------------------
+// SSE correction (corr: the residuals in the SSE slot were taken to the fp32
+// image c' = (float) c of each centroid -- k_s1's delta fit with compute_sse):
+// per cluster sum ||x - c||^2 - sum ||x - c'||^2 = sum_f dl_f (n dl_f -
+// 2 (S_f - n c'_f)), dl = c - c', exact as an identity; its rounding is
+// ~2^-53 of the term, which is ~2^-24 of the cluster's share (DESIGN.md
+// section 2 "Statistics and SSE").  Returns the lane's share.
+__device__ __forceinline__ double sse_corr_term(double o, double S, double cnt) {
+  const double cp = (double)(float)o;
+  const double dl = o - cp;
+  return dl * fma(cnt, dl, -2.0 * fma(-cnt, cp, S));
+}
+
 __global__ __launch_bounds__(64) void k_update(const double* __restrict__ stats, const double* __restrict__ old,
                                                int k, int d, double* __restrict__ out, double* __restrict__ work,
-                                               int64_t* __restrict__ counts, const int* __restrict__ gate) {
+                                               int64_t* __restrict__ counts, const int* __restrict__ gate, int corr) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   const int j = blockIdx.x;
   const int lane = threadIdx.x;
   const int d1 = d + 1;
   const double cnt = stats[(size_t)j * d1 + d];
-  double sh = 0.0, nf = 0.0;
+  double sh = 0.0, nf = 0.0, cr = 0.0;
   for (int f = lane; f < d; f += 64) {
     const double S = stats[(size_t)j * d1 + f];
     const double o = old[(size_t)j * d + f];
@@ -4682,11 +4715,14 @@ __global__ __launch_bounds__(64) void k_update(const double* __restrict__ stats,
     const double df = nv - o;
     sh = fma(df, df, sh);
     if (!isfinite(nv)) nf = 1.0;
+    if (corr) cr += sse_corr_term(o, S, cnt);
   }
   sh = wave_sum(sh);
   nf = wave_sum(nf);
+  if (corr) cr = wave_sum(cr);
   if (lane == 0) {
     work[j] = sh;
+    work[k + j] = cr;
     work[2 * k + j] = nf;
     counts[j] = (int64_t)cnt;
   }
@@ -4701,7 +4737,8 @@ __global__ __launch_bounds__(64) void k_update(const double* __restrict__ stats,
 __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ work, const int64_t* __restrict__ counts,
                                                   int k, const double* __restrict__ sse,
                                                   const uint32_t* __restrict__ qcount, uint32_t nq,
-                                                  DevStatus* __restrict__ st, int* __restrict__ gate, double stop_tol, int dev_repair) {
+                                                  DevStatus* __restrict__ st, int* __restrict__ gate, double stop_tol, int dev_repair,
+                                                  int corr) {
   if (*gate) {
     if (threadIdx.x == 0) {
       st->ran = 0;
@@ -4709,9 +4746,9 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ wor
     }
     return;
   }
-  __shared__ double s_max[256];
+  __shared__ double s_max[256], s_cr[256];
   __shared__ int s_emp[256], s_nf[256], s_q[256], s_qf[256];
-  double mx = 0.0;
+  double mx = 0.0, cr = 0.0;
   int emp = 0, nf = 0, qa = 0, qb = 0;
   for (uint32_t w = threadIdx.x; w < nq; w += 256) {
     qa += (int)qcount[2 * w];
@@ -4723,14 +4760,17 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ wor
     mx = fmax(mx, work[j]);
     nf |= (work[2 * k + j] != 0.0);
     emp += (counts[j] == 0);
+    if (corr) cr += work[k + j];
   }
   s_max[threadIdx.x] = mx;
+  s_cr[threadIdx.x] = cr;
   s_emp[threadIdx.x] = emp;
   s_nf[threadIdx.x] = nf;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if (threadIdx.x < o) {
       s_max[threadIdx.x] = fmax(s_max[threadIdx.x], s_max[threadIdx.x + o]);
+      s_cr[threadIdx.x] += s_cr[threadIdx.x + o];
       s_emp[threadIdx.x] += s_emp[threadIdx.x + o];
       s_nf[threadIdx.x] |= s_nf[threadIdx.x + o];
       s_q[threadIdx.x] += s_q[threadIdx.x + o];
@@ -4741,7 +4781,7 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ wor
   if (threadIdx.x == 0) {
     const double ms = sqrt(s_max[0]);
     st->max_shift = ms;
-    st->sse = *sse;
+    st->sse = corr ? *sse + s_cr[0] : *sse;
     st->n_empty = s_emp[0];
     st->nonfinite = s_nf[0];
     st->q_full = s_qf[0];
@@ -4780,24 +4820,24 @@ __device__ void update_one_body(double* __restrict__ stats, const double* __rest
                                 double* __restrict__ out, int64_t* __restrict__ counts, const double* __restrict__ sse,
                                 const uint32_t* __restrict__ qcount, uint32_t nq, DevStatus* __restrict__ st,
                                 int* __restrict__ gate, double stop_tol, int dev_repair, int clear,
-                                float* __restrict__ C32, float* __restrict__ cmax, int dp, int kp) {
+                                float* __restrict__ C32, float* __restrict__ cmax, int dp, int kp, int corr) {
   auto ld = [](const double* p) {
     if constexpr (COHERENT)
       return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else
       return *p;
   };
-  __shared__ double s_max[16];
+  __shared__ double s_max[16], s_cr[16];
   __shared__ int s_emp[16], s_nf[16], s_q[16], s_qf[16];
   __shared__ unsigned int s_cm[16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int d1 = d + 1;
-  double mx = 0.0;
+  double mx = 0.0, crs = 0.0;
   int emp = 0, nf = 0, qa = 0, qb = 0;
   unsigned int cmb = 0u;  // max ||c|| bits (k_prep_small)
   for (int j = wave; j < k; j += nw) {
     const double cnt = ld(stats + (size_t)j * d1 + d);
-    double sh = 0.0, nfl = 0.0, nn = 0.0;
+    double sh = 0.0, nfl = 0.0, nn = 0.0, cr = 0.0;
     for (int f = lane; f < (C32 ? dp : d); f += 64) {
       if (f < d) {
         const double S = ld(stats + (size_t)j * d1 + f);
@@ -4807,6 +4847,7 @@ __device__ void update_one_body(double* __restrict__ stats, const double* __rest
         const double df = nv - o;
         sh = fma(df, df, sh);
         if (!isfinite(nv)) nfl = 1.0;
+        if (corr) cr += sse_corr_term(o, S, cnt);
         if (C32) {
           nn = fma(nv, nv, nn);
           C32[(size_t)j * dp + f] = (float)nv;
@@ -4819,7 +4860,9 @@ __device__ void update_one_body(double* __restrict__ stats, const double* __rest
     sh = wave_sum(sh);
     nfl = wave_sum(nfl);
     if (C32) nn = wave_sum(nn);
+    if (corr) cr = wave_sum(cr);
     if (lane == 0) {
+      crs += cr;
       counts[j] = (int64_t)cnt;
       mx = fmax(mx, sh);
       nf |= (nfl != 0.0);
@@ -4839,6 +4882,7 @@ __device__ void update_one_body(double* __restrict__ stats, const double* __rest
   }
   if (lane == 0) {
     s_max[wave] = mx;
+    s_cr[wave] = crs;
     s_emp[wave] = emp;
     s_nf[wave] = nf;
     s_q[wave] = qa;
@@ -4852,6 +4896,7 @@ __device__ void update_one_body(double* __restrict__ stats, const double* __rest
     for (int i = threadIdx.x; i < k * d1 + 1; i += blockDim.x) stats[i] = 0.0;
   if (threadIdx.x == 0) {
     for (int w = 1; w < nw; ++w) {
+      crs += s_cr[w];
       mx = fmax(mx, s_max[w]);
       emp += s_emp[w];
       nf |= s_nf[w];
@@ -4862,7 +4907,7 @@ __device__ void update_one_body(double* __restrict__ stats, const double* __rest
     if (C32) *cmax = __uint_as_float(cmb);
     const double ms = sqrt(mx);
     st->max_shift = ms;
-    st->sse = sse_v;
+    st->sse = corr ? sse_v + crs : sse_v;
     st->n_empty = emp;
     st->nonfinite = nf;
     st->q_full = qb;
@@ -4889,7 +4934,7 @@ __global__ __launch_bounds__(1024) void k_update_one(double* __restrict__ stats,
                                                      const uint32_t* __restrict__ qcount, uint32_t nq,
                                                      DevStatus* __restrict__ st, int* __restrict__ gate,
                                                      double stop_tol, int dev_repair, int clear, float* __restrict__ C32,
-                                                     float* __restrict__ cmax, int dp, int kp) {
+                                                     float* __restrict__ cmax, int dp, int kp, int corr) {
   if (*gate) {
     if (threadIdx.x == 0) {
       st->ran = 0;
@@ -4898,7 +4943,7 @@ __global__ __launch_bounds__(1024) void k_update_one(double* __restrict__ stats,
     return;
   }
   update_one_body<false>(stats, old, k, d, out, counts, sse, qcount, nq, st, gate, stop_tol, dev_repair, clear, C32,
-                         cmax, dp, kp);
+                         cmax, dp, kp, corr);
 }
 
 bool update_one_ok(const Geometry& g) { return g.k <= 64 && (size_t)g.k * g.d <= 16384; }
@@ -4906,19 +4951,20 @@ bool update_one_ok(const Geometry& g) { return g.k <= 64 && (size_t)g.k * g.d <=
 hipError_t launch_update(double* stats, const double* C64_old, const Geometry& g, double* C64_new,
                          double* work, int64_t* counts, const uint32_t* qcount, uint32_t nq, DevStatus* status,
                          int* gate, double stop_tol, int dev_repair, hipStream_t s, int clear, float* C32,
-                         float* cmax) {
+                         float* cmax, int corr) {
   if (update_one_ok(g)) {  // at most 4 clusters per wave (c3: 2 launches, 11 vs 37 us)
     hipLaunchKernelGGL(k_update_one, dim3(1), dim3(1024), 0, s, stats, C64_old, g.k, g.d, C64_new, counts,
                        stats + (size_t)g.k * (g.d + 1), qcount, nq, status, gate, stop_tol, dev_repair, clear, C32,
-                       cmax, g.dp, g.kp);
+                       cmax, g.dp, g.kp, corr);
     return hipGetLastError();
   }
   if (clear || C32) return hipErrorInvalidValue;  // only the one-workgroup update clears / prepares
-  hipLaunchKernelGGL(k_update, dim3(g.k), dim3(64), 0, s, stats, C64_old, g.k, g.d, C64_new, work, counts, gate);
+  hipLaunchKernelGGL(k_update, dim3(g.k), dim3(64), 0, s, stats, C64_old, g.k, g.d, C64_new, work, counts, gate,
+                     corr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, work, counts, g.k, stats + (size_t)g.k * (g.d + 1),
-                     qcount, nq, status, gate, stop_tol, dev_repair);
+                     qcount, nq, status, gate, stop_tol, dev_repair, corr);
   return hipGetLastError();
 }
 

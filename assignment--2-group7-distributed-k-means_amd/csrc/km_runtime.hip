@@ -108,6 +108,7 @@ struct km_ctx {
   bool sweep_rev = false;        // the last k_assign_small / k_s1 launch swept the rows last-first
   int stats_pending = 0;         // the last assign left 0 nothing, 1 full sums, 2 deltas in stats
   bool last_delta = false;       // the last assign with statistics left deltas (km_info.delta_stats)
+  bool sse_corr = false;         // the pending SSE slot holds residuals to the fp32 images c' (update corrects)
   float* bal = nullptr;  // fast screen: image error maxima (2 floats)
   // statistics already zero (the batch update cleared them): no memset
   bool stats_clean = false;
@@ -478,13 +479,15 @@ bool one_screen(km_ctx* c) {
 }
 
 // k_s1 for this assign: labels only (predict), or delta statistics once the
-// labels and the full sums of a previous iteration are in place (no SSE: its
-// residuals need every row; and only where k_s1_delta's table fits LDS)
+// labels and the full sums of a previous iteration are in place (with
+// compute_sse k_s1 also adds every row's residual to the fp32 image of its
+// centroid, the resolvers the queued rows', and the update corrects the total
+// to the exact SSE: every row is read once either way)
 bool use_s1(km_ctx* c, bool with_stats) {
   if (!c->s1) return false;
   if (c->screen_forced >= 0 && c->screen_forced != KM_SCREEN_S1) return false;
   // (a caller that took the buffer with km_stats_buffer reads full sums)
-  return !with_stats || (c->delta_ready && !c->want_sse && !c->stats_exported && km::s1_delta_ok(c->g, c->n_cu));
+  return !with_stats || (c->delta_ready && !c->stats_exported && km::s1_delta_ok(c->g, c->n_cu));
 }
 
 // before an update reads the statistics: delta -> fold into the full sums;
@@ -497,7 +500,9 @@ int apply_stats(km_ctx* c, const double** upd_src = nullptr, bool clear = false)
   c->stats_pending = 0;
   if (upd_src) *upd_src = c->stats;
   if (!c->s1) return KM_OK;
-  const bool keep = kind == 2 || (kind == 1 && !c->want_sse);
+  // full sums (kind 1) become the base of the next deltas, the deltas
+  // (kind 2) are folded into them (k_s1_apply replaces the SSE slot)
+  const bool keep = kind == 2 || kind == 1;
   const bool zero = kind == 2 && clear && upd_src;
   if (keep)
     KM_HIP(km::launch_s1_apply(c->stats, c->stats_full, (int64_t)stats_len(c->g), kind == 2 ? (zero ? 2 : 1) : 0,
@@ -508,6 +513,14 @@ int apply_stats(km_ctx* c, const double** upd_src = nullptr, bool clear = false)
   }
   c->delta_ready = keep;
   return KM_OK;
+}
+
+// the SSE correction flag of the statistics an update is about to read
+// (consumed once)
+int take_sse_corr(km_ctx* c) {
+  const bool v = c->sse_corr;
+  c->sse_corr = false;
+  return v ? 1 : 0;
 }
 
 // a deferred km_assign_stats launched on its own (any call but km_update_async
@@ -549,13 +562,17 @@ int run_assign(km_ctx* c, bool with_stats) {
   if (with_stats) {
     c->stats_pending = 1;
     c->last_delta = false;
+    c->sse_corr = false;
   }
   if (use_s1(c, with_stats)) {
+    // compute_sse with delta statistics: residuals to the fp32 images c'
+    // (k_s1, the resolvers), corrected by the update (km::launch_update corr)
+    double* s1_sse = sse ? sse_slot : nullptr;
     {
       ProfScope ps(c, KM_K_ASSIGN, true);
       KM_HIP(km::launch_s1(c->X, c->xnorm, g, c->s1_img, c->s1_cn2o, c->s1_cft, c->s1_perm, c->s1_cst,
                            c->labels, c->queue, c->qcount, c->chg, c->chg_cnt, with_stats ? 1 : 0, c->n_cu,
-                           &c->ql, c->gate, c->stream, next_sweep(c)));
+                           &c->ql, c->gate, c->stream, next_sweep(c), s1_sse));
     }
     {
       // the queued rows: near-ties of the re-scored candidates and the rows
@@ -563,8 +580,8 @@ int run_assign(km_ctx* c, bool with_stats) {
       // still hold their previous labels)
       ProfScope ps(c, KM_K_RESOLVE);
       KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels,
-                                with_stats ? c->stats : nullptr, c->n_cu, c->gate, c->stream, nullptr, nullptr, 0,
-                                with_stats ? 1 : 0));
+                                with_stats ? c->stats : nullptr, c->n_cu, c->gate, c->stream, s1_sse, nullptr, 0,
+                                with_stats ? 1 : 0, s1_sse ? c->C32 : nullptr));
     }
     if (with_stats) {
       // the rows k_s1 moved between clusters (its change list) into the deltas
@@ -574,6 +591,7 @@ int run_assign(km_ctx* c, bool with_stats) {
     if (with_stats) {
       c->stats_pending = 2;
       c->last_delta = true;
+      c->sse_corr = s1_sse != nullptr;
     }
     return KM_OK;
   }
@@ -1086,7 +1104,8 @@ int km_update(km_ctx* c, km_status* st, int64_t* counts) {
   {
     ProfScope ps(c, KM_K_UPDATE);
     KM_HIP(km::launch_update(const_cast<double*>(src), c->C64_cur, c->g, c->C64_new, c->work, c->counts_dev, c->qcount,
-                             c->ql.nwaves, c->status_dev, c->gate, -1.0, 0, c->stream));
+                             c->ql.nwaves, c->status_dev, c->gate, -1.0, 0, c->stream, 0, nullptr, nullptr,
+                             take_sse_corr(c)));
   }
   KM_HIP(hipMemcpyAsync(c->status_host, c->status_dev, sizeof(km::DevStatus), hipMemcpyDeviceToHost, c->stream));
   KM_HIP(hipMemcpyAsync(c->counts_host, c->counts_dev, sizeof(int64_t) * c->g.k, hipMemcpyDeviceToHost, c->stream));
@@ -1231,7 +1250,7 @@ int km_update_async(km_ctx* c, double tol, int64_t empty_seed) {
     KM_HIP(km::launch_update(one ? c->stats : const_cast<double*>(src), c->C64_cur, c->g, c->C64_new, c->work,
                              c->hist_counts + (size_t)slot * c->g.k, c->qcount, c->ql.nwaves, c->hist + slot,
                              c->gate, tol, repair ? 1 : 0, c->stream, one ? 1 : 0, fold_prep ? c->C32 : nullptr,
-                             fold_prep ? c->cmax : nullptr));
+                             fold_prep ? c->cmax : nullptr, take_sse_corr(c)));
   }
   if (one) c->stats_clean = true;
   if (repair) {

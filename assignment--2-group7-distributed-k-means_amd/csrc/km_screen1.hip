@@ -328,6 +328,7 @@ struct S1Args {
   uint32_t* qcount;
   uint2* chg;          // DELTA: changed rows {row, old << 16 | new}, [wave][seg]
   uint32_t* chg_cnt;   // DELTA: entries per wave segment
+  double* sse;         // SSE (MODE 1): every decided row's residual to the fp32 image c' of its centroid
   const int* gate;
 };
 
@@ -335,7 +336,14 @@ struct S1Args {
 // rows' by the resolvers).  MODE 1: delta statistics (the previous labels are
 // read; only changed labels are written and moved in the sums; queued rows
 // keep their previous label for the resolvers to compare).
-template <int NS2, int NB, int MODE, bool REV = false>
+// SSE (MODE 1 only, compute_sse with delta statistics): every row the kernel
+// decides adds sum_f (x_f - c'_f)^2 in float64 (fp32 x and c' are exact in
+// float64) for c' = the fp32 image of its centroid, from the table it
+// re-scores with; the resolvers add the queued rows' the same way
+// (launch_resolve sse_c32), and the update turns the total into
+// sum ||x - c||^2 with one exact per-cluster correction from the full sums
+// (k_update, sse_corr; DESIGN.md section 2 "Statistics and SSE").
+template <int NS2, int NB, int MODE, bool REV = false, bool SSE = false>
 __global__ __launch_bounds__(s1_waves(NS2, NB) * 64, s1_waves(NS2, NB) / 4) void k_s1(S1Args A) {
   if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   constexpr int S1_WAVES = s1_waves(NS2, NB);
@@ -391,6 +399,32 @@ __global__ __launch_bounds__(s1_waves(NS2, NB) * 64, s1_waves(NS2, NB) / 4) void
   QEntry* wq = A.queue + (size_t)gw * A.seg;
   uint2* wc = A.chg + (size_t)gw * A.seg;
   uint32_t qn = 0, qf = 0, cc = 0;
+  double ssa = 0.0;  // SSE: this lane's share of its decided rows' residuals
+  // SSE: the lane's features of a decided row against table slot `slot`
+  auto resid = [&](bool act, uint32_t slot, const float4* xv) {
+    if constexpr (SSE) {
+      const uint32_t sl = act ? slot : 0u;
+      const float4* cp = TG ? reinterpret_cast<const float4*>(A.cft + sl * CS + FQ * q)
+                            : reinterpret_cast<const float4*>(sCf + sl * CS + FQ * q);
+      double r = 0.0;
+#pragma unroll
+      for (int u = 0; u < FQ / 4; ++u) {
+        const float4 c = cp[u];
+        const float4 x = xv[u];
+        const double e0 = (double)x.x - (double)c.x, e1 = (double)x.y - (double)c.y;
+        const double e2 = (double)x.z - (double)c.z, e3 = (double)x.w - (double)c.w;
+        r = fma(e0, e0, r);
+        r = fma(e1, e1, r);
+        r = fma(e2, e2, r);
+        r = fma(e3, e3, r);
+      }
+      ssa += act ? r : 0.0;
+    } else {
+      (void)act;
+      (void)slot;
+      (void)xv;
+    }
+  };
   // chain id bits of this lane's 8 accumulator positions (cb, i): chain 16 cb + 4 q + i
   const uint32_t qbits = (uint32_t)(4 * q) << MB;
 
@@ -425,7 +459,7 @@ __global__ __launch_bounds__(s1_waves(NS2, NB) * 64, s1_waves(NS2, NB) / 4) void
   // hardware sqrt loses accuracy: U takes sqrt(2^-96) (an over-estimate), L
   // takes 0 (an under-estimate)
   auto decide = [&](bool act0, uint32_t cnt, const uint32_t* sl, const float4* xv, int32_t& lab1, int32_t& lab2,
-                    uint32_t& kind) {
+                    uint32_t& kind, uint32_t& ws) {
     auto partial = [&](uint32_t slot) {
       const float4* cp = TG ? reinterpret_cast<const float4*>(A.cft + slot * CS + FQ * q)
                             : reinterpret_cast<const float4*>(sCf + slot * CS + FQ * q);
@@ -492,6 +526,7 @@ __global__ __launch_bounds__(s1_waves(NS2, NB) * 64, s1_waves(NS2, NB) / 4) void
       lab1 = l1;
       lab2 = l2;
       kind = kd;
+      ws = s1;  // the winner's table slot (SSE residual)
     }
   };
   // a row's outcome (every lane of its quad calls with the same values):
@@ -570,9 +605,10 @@ __global__ __launch_bounds__(s1_waves(NS2, NB) * 64, s1_waves(NS2, NB) / 4) void
         }
       }
       int32_t lab1 = 0, lab2 = 0;
-      uint32_t kind = 2u;
-      decide(act, cnt, sl, xv, lab1, lab2, kind);
+      uint32_t kind = 2u, ws = 0u;
+      decide(act, cnt, sl, xv, lab1, lab2, kind, ws);
       emit(act, mt.x, kind, lab1, lab2, (int32_t)(mt.y & 0xFFFFu));
+      resid(act && kind == 0u, ws, xv);
     } else {
       (void)nb;
     }
@@ -668,6 +704,7 @@ __global__ __launch_bounds__(s1_waves(NS2, NB) * 64, s1_waves(NS2, NB) / 4) void
 #endif
     if constexpr (BATCH) {
       emit(valid && !needy, row, dec1 ? 0u : 2u, labm, 0, old);
+      resid(dec1, sm, B.x);
       // rows with 2..LMAX candidates: into the wave's ring with their
       // smallest head and every chain head, from which the batch extracts the
       // rest; a full ring is re-scored as one batch
@@ -715,9 +752,10 @@ __global__ __launch_bounds__(s1_waves(NS2, NB) * 64, s1_waves(NS2, NB) / 4) void
         sl[r] = f2u(prev) & SLOTM;
       }
       int32_t lab1 = labm, lab2 = 0;
-      uint32_t kind = dec1 ? 0u : 2u;
-      if (__ballot(needy) != 0ull) decide(needy, cnt, sl, B.x, lab1, lab2, kind);
+      uint32_t kind = dec1 ? 0u : 2u, ws = sm;
+      if (__ballot(needy) != 0ull) decide(needy, cnt, sl, B.x, lab1, lab2, kind, ws);
       emit(valid, row, kind, lab1, lab2, old);
+      resid(valid && kind == 0u, ws, B.x);
     }
   };
 
@@ -921,6 +959,11 @@ __global__ __launch_bounds__(s1_waves(NS2, NB) * 64, s1_waves(NS2, NB) / 4) void
     A.qcount[2 * gw + 1] = qf;
     if constexpr (MODE == 1) A.chg_cnt[gw] = cc;
   }
+  if constexpr (SSE) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) ssa += __shfl_xor(ssa, o);
+    if (lane == 0 && ssa != 0.0) atomicAdd(A.sse, ssa);
+  }
 }
 
 // Delta statistics (km_runtime.hip): mode 1 folds an iteration's all-reduced
@@ -935,7 +978,9 @@ __global__ __launch_bounds__(256) void k_s1_apply(double* __restrict__ stats, do
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= len) return;
   double v = stats[i];
-  if (mode >= 1) v = full[i] + v;
+  // (the SSE slot, the last entry, is this iteration's residual sum, never
+  // carried: it is replaced, not added)
+  if (mode >= 1 && i != len - 1) v = full[i] + v;
   full[i] = v;
   stats[i] = mode == 2 ? 0.0 : v;
 }
@@ -953,14 +998,19 @@ __global__ __launch_bounds__(256) void k_s1_apply(double* __restrict__ stats, do
 #endif
 constexpr uint32_t S1D_MIN = KM_S1D_MIN;
 constexpr int S1D_ROWS = 8;
+// DIRECT (the table does not fit LDS: c4 class, k (d + 1) doubles > 160 KiB):
+// each changed row goes straight to the statistics with float64 global
+// atomics (few rows change in steady state).
+template <bool DIRECT>
 __global__ __launch_bounds__(1024) void k_s1_delta(const float* __restrict__ X, int dp, int d, int k,
                                                    const uint2* __restrict__ chg, const uint32_t* __restrict__ cnt,
                                                    int nw, uint32_t seg, double* __restrict__ stats,
                                                    const int* __restrict__ gate) {
   if (*gate) return;
-  extern __shared__ double tab[];  // [k][d + 1], then pre[nw + 1]
+  extern __shared__ double smem_d[];  // [k][d + 1] (not DIRECT), then pre[nw + 1]
   const int d1 = d + 1;
-  uint32_t* pre = reinterpret_cast<uint32_t*>(tab + (size_t)k * d1);
+  double* tab = DIRECT ? stats : smem_d;
+  uint32_t* pre = reinterpret_cast<uint32_t*>(smem_d + (DIRECT ? 0 : (size_t)k * d1));
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   if (wave == 0) {
     uint32_t run = 0;
@@ -983,7 +1033,8 @@ __global__ __launch_bounds__(1024) void k_s1_delta(const float* __restrict__ X, 
   const uint32_t e0 = blockIdx.x * per;
   if (e0 >= nc) return;
   const uint32_t e1 = min(nc, e0 + per);
-  for (int i = threadIdx.x; i < k * d1; i += blockDim.x) tab[i] = 0.0;
+  if constexpr (!DIRECT)
+    for (int i = threadIdx.x; i < k * d1; i += blockDim.x) tab[i] = 0.0;
   __syncthreads();
   // entry e of the concatenation: segment w = the last with pre[w] <= e
   auto at = [&](uint32_t e) {
@@ -1022,10 +1073,12 @@ __global__ __launch_bounds__(1024) void k_s1_delta(const float* __restrict__ X, 
         atomicAdd(tab + (size_t)(c[r].y & 0xFFFFu) * d1 + d, 1.0);
       }
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < k * d1; i += blockDim.x) {
-    const double v = tab[i];
-    if (v != 0.0) atomicAdd(stats + i, v);
+  if constexpr (!DIRECT) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < k * d1; i += blockDim.x) {
+      const double v = tab[i];
+      if (v != 0.0) atomicAdd(stats + i, v);
+    }
   }
 }
 
@@ -1064,7 +1117,13 @@ size_t s1_wave_slots(int n_cu) { return (size_t)n_cu * S1_MAX_WAVES; }
 static size_t s1_delta_lds(const Geometry& g, int n_cu) {
   return (size_t)g.k * (g.d + 1) * 8 + ((size_t)n_cu * s1_geo_waves(g) + 1) * 4;
 }
-bool s1_delta_ok(const Geometry& g, int n_cu) { return s1_delta_lds(g, n_cu) <= 160 * 1024 && g.k <= 65535; }
+// the LDS aggregation fits; otherwise k_s1_delta<DIRECT> (global atomics).
+// Every k_s1 geometry has delta statistics (k < 65536: 16-bit cluster ids)
+static bool s1_delta_lds_ok(const Geometry& g, int n_cu) { return s1_delta_lds(g, n_cu) <= 160 * 1024; }
+bool s1_delta_ok(const Geometry& g, int n_cu) {
+  (void)n_cu;
+  return g.k <= 65535;
+}
 
 hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt,
                            double* stats, int n_cu, const int* gate, hipStream_t s) {
@@ -1072,10 +1131,15 @@ hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, 
   int nbk;
   uint32_t seg;
   const int64_t nw = s1_grid(g, n_cu, &nbk, &seg);
-  const size_t lds = s1_delta_lds(g, n_cu);  // (nw <= n_cu * waves)
   if (!s1_delta_ok(g, n_cu)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_s1_delta, dim3(n_cu), dim3(1024), lds, s, X, g.dp, g.d, g.k, chg, chg_cnt, (int)nw, seg, stats,
-                     gate);
+  if (s1_delta_lds_ok(g, n_cu)) {
+    const size_t lds = s1_delta_lds(g, n_cu);  // (nw <= n_cu * waves)
+    hipLaunchKernelGGL(k_s1_delta<false>, dim3(n_cu), dim3(1024), lds, s, X, g.dp, g.d, g.k, chg, chg_cnt, (int)nw,
+                       seg, stats, gate);
+  } else {
+    hipLaunchKernelGGL(k_s1_delta<true>, dim3(n_cu), dim3(1024), ((size_t)nw + 1) * 4, s, X, g.dp, g.d, g.k, chg,
+                       chg_cnt, (int)nw, seg, stats, gate);
+  }
   return hipGetLastError();
 }
 
@@ -1144,7 +1208,7 @@ hipError_t launch_s1_prep(const double* C64, const float* C32, const Geometry& g
 hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, const uint4* img, const float* cn2o,
                      const float* cft, const int32_t* perm, const float* cst, int32_t* labels,
                      QEntry* queue, uint32_t* qcount, uint2* chg, uint32_t* chg_cnt, int delta, int n_cu,
-                     QLayout* ql, const int* gate, hipStream_t s, int rev) {
+                     QLayout* ql, const int* gate, hipStream_t s, int rev, double* sse) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
@@ -1155,13 +1219,16 @@ hipError_t launch_s1(const float* X, const float* xnorm, const Geometry& g, cons
   const int64_t nw = s1_grid(g, n_cu, &nbk, &seg);
   ql->seg = seg;
   ql->nwaves = (uint32_t)nw;
-  S1Args a{X, xnorm, g.n, g.k, g.d, seg, img, cn2o, cft, perm, cst, labels, queue, qcount, chg, chg_cnt, gate};
+  if (sse && !delta) return hipErrorInvalidValue;  // residuals ride with delta statistics only
+  S1Args a{X, xnorm, g.n, g.k, g.d, seg, img, cn2o, cft, perm, cst, labels, queue, qcount, chg, chg_cnt, sse, gate};
   const size_t lds = s1_lds_bytes(sg.ns2, sg.nb, !s1_table_global(sg.ns2, sg.nb));
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   (void)nt;
 #define KM_S1_CASE(NS2_, NB_)                                                                                   \
   case NS2_ * 100 + NB_:                                                                                        \
-    if (delta && rev && KM_S1_SERP && NS2_ == 2 && NB_ == 8)                                                    \
+    if (delta && sse)                                                                                           \
+      KM_TIMED_LAUNCH((k_s1<NS2_, NB_, 1, false, true>), dim3(nbk), dim3(s1_waves(NS2_, NB_) * 64), lds, s, a); \
+    else if (delta && rev && KM_S1_SERP && NS2_ == 2 && NB_ == 8)                                               \
       KM_TIMED_LAUNCH((k_s1<2, 8, 1, true>), dim3(nbk), dim3(s1_waves(2, 8) * 64), lds, s, a);                  \
     else if (delta)                                                                                             \
       KM_TIMED_LAUNCH((k_s1<NS2_, NB_, 1>), dim3(nbk), dim3(s1_waves(NS2_, NB_) * 64), lds, s, a);              \

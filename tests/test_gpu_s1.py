@@ -342,22 +342,23 @@ def test_long_delta_fit_no_drift_vs_full_statistics():
     np.testing.assert_array_equal(ea.predict(), orc.assign(X, C_prev)[0])
 
 
-@pytest.mark.parametrize("n,d,k,centers,delta", [
-    (20000, 18, 1000, 300, True),    # dp 32, kp 1024 (unfused): k (d+1) 8 + the wave prefix fits LDS
-    (20000, 19, 1000, 300, False),   # dp 32, kp 1024: 160,000 B of table + the prefix do not fit
-    (20000, 60, 480, 200, False),    # dp 64, kp 512 (unfused): the table does not fit -> full statistics
+@pytest.mark.parametrize("n,d,k,centers", [
+    (20000, 18, 1000, 300),   # dp 32, kp 1024 (unfused): k (d+1) 8 + the wave prefix fit LDS -> LDS aggregation
+    (20000, 19, 1000, 300),   # dp 32, kp 1024: 160,000 B of table + the prefix do not fit -> direct atomics
+    (20000, 60, 480, 200),    # dp 64, kp 512 (unfused): direct atomics
 ])
-def test_unfused_geometries_delta_statistics(n, d, k, centers, delta):
-    # the unfused k_s1 geometries take delta statistics where the [k][d+1]
-    # table and the largest grid's wave prefix fit LDS (km_screen1.hip
-    # s1_delta_ok: geometry and device only); their changed rows are resolved
-    # by the direct-atomic k_rerank2 / k_fullscan paths
+def test_unfused_geometries_delta_statistics(n, d, k, centers):
+    # every k_s1 geometry takes delta statistics (round 6): k_s1_delta
+    # aggregates the changed rows in an LDS [k][d+1] table where it fits
+    # beside the largest grid's wave prefix (geometry and device only, never
+    # the rank's rows), else with direct float64 atomics; the resolvers move
+    # their changed rows with direct atomics
     X = _blobs(n, d, centers, seed=21 + k + d)
     C0 = X[np.random.default_rng(22).choice(n, k, replace=False)]
     km = _check_fit(X, C0, 5)
     info = km._runner.engine.info()
     assert info["fused_stats"] == 0
-    assert info["delta_stats"] == (1 if delta else 0)
+    assert info["delta_stats"] == 1
 
 
 def test_assign_stats_twice_before_update():
@@ -402,14 +403,46 @@ def test_predict_between_assign_and_update_keeps_the_deltas():
     np.testing.assert_allclose(eng.get_centroids(1), ref["centroids"], rtol=1e-9, atol=1e-9)
 
 
-def test_compute_sse_keeps_full_statistics():
+def test_compute_sse_with_delta_statistics():
+    # compute_sse no longer forces full statistics (round 6): from the second
+    # iteration k_s1 adds every decided row's float64 residual to the fp32
+    # image c' of its centroid, the resolvers the queued rows', and the update
+    # adds the exact per-cluster correction -2 dl (S - n c') + n dl^2
+    # (dl = c - c'), so the SSE is the reference's sum of min(norm)**2
+    # (kmeans_spark.py:224-237) with one read of the rows per iteration
     X = _blobs(20000, 64, 256, seed=51)
     C0 = X[np.random.default_rng(52).choice(len(X), 256, replace=False)]
-    km = _fit(X, C0, 3, compute_sse=True)
-    assert km._runner.engine.screen() != S1
-    ref = orc.lloyd_fit(X, 256, 3, 1e-12, 0, True, 1, init_centroids=C0, empty_seed=lambda: SEED)
+    km = _fit(X, C0, 4, compute_sse=True)
+    eng = km._runner.engine
+    assert eng.screen() == S1 and eng.info()["delta_stats"] == 1
+    ref = orc.lloyd_fit(X, 256, 4, 1e-12, 0, True, 1, init_centroids=C0, empty_seed=lambda: SEED)
     np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
     np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)
+
+
+@pytest.mark.parametrize("n,d,k,centers", [
+    (12000, 64, 256, 64),     # c3 geometry: LDS delta table, fp32 table in LDS
+    (12000, 32, 1024, 256),   # c4 geometry: direct-atomic deltas, fp32 table in global memory
+])
+def test_tight_clusters_sse_delta_iterations(n, d, k, centers):
+    # std 1e-3 in a +-1000 box (sum ||x||^2 ~ 1e12 x the SSE): the residuals to
+    # c' and the per-cluster correction must hold 1e-9 where any closed form
+    # through ||x||^2 cancels; the screen's bound is wide here, so most rows
+    # reach the float64 resolvers, which add their residuals the same way
+    rng = np.random.default_rng(d + k)
+    C = rng.uniform(-1000, 1000, (centers, d))
+    blob = rng.integers(0, centers, n)
+    X = (C[blob] + 1e-3 * rng.standard_normal((n, d))).astype(np.float32).astype(np.float64)
+    first = [int(np.nonzero(blob == b)[0][0]) for b in range(centers) if np.any(blob == b)]
+    rest = np.setdiff1d(np.arange(n), first)
+    C0 = X[np.concatenate([first, rng.choice(rest, k - len(first), replace=False)]).astype(np.int64)]
+    km = _fit(X, C0, 4, compute_sse=True)
+    eng = km._runner.engine
+    assert eng.screen() == S1 and eng.info()["delta_stats"] == 1
+    ref = orc.lloyd_fit(X, k, 4, 1e-12, 0, True, 1, init_centroids=C0, empty_seed=lambda: SEED)
+    assert ref["sse_history"][-1] < 1e-4 * np.sum(X * X)
+    np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)
+    np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
 
 
 # -- the unfused geometries (c4 class): k_s1 labels, then the statistics pass ------------
@@ -417,14 +450,15 @@ def test_compute_sse_keeps_full_statistics():
 @pytest.mark.parametrize("compute_sse", [True, False])
 def test_fit_c4_shape_labels_then_statistics_pass(compute_sse):
     # k = 1024, d = 32 (c4's geometry; BASELINE configs[3] has compute_sse on):
-    # no fused statistics table fits, so k_s1 writes every label and the
-    # statistics pass (with the SSE residuals) reads X again; the delta table
-    # [k][d+1] f64 does not fit LDS either, so every iteration is full
+    # no fused statistics table fits, so the first iteration is k_s1's labels
+    # and the statistics pass (with the SSE residuals); from the second on,
+    # delta statistics with direct float64 atomics (the [k][d+1] table does
+    # not fit LDS) and the residuals in k_s1: one read of X per iteration
     X = _blobs(30000, 32, 1024, seed=61)
     C0 = X[np.random.default_rng(62).choice(len(X), 1024, replace=False)]
     km = _fit(X, C0, 4, compute_sse=compute_sse)
     eng = km._runner.engine
-    assert eng.screen() == S1
+    assert eng.screen() == S1 and eng.info()["delta_stats"] == 1
     ref = orc.lloyd_fit(X, 1024, 4, 1e-12, 0, compute_sse, 1, init_centroids=C0, empty_seed=lambda: SEED)
     np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
     if compute_sse:
