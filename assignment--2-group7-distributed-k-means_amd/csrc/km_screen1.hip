@@ -80,7 +80,12 @@ constexpr int ceil_log2_c(int v) { return v <= 1 ? 0 : 1 + ceil_log2_c((v + 1) /
 #ifndef KM_S1_W12
 #define KM_S1_W12 1
 #endif
-constexpr int s1_waves(int ns2, int nb) { return (KM_S1_W12 && ns2 == 2 && nb == 8) ? 12 : 8; }
+#ifndef KM_S1_W12_C4  // the same on the c4 geometry (dp 32, kp 1024)
+#define KM_S1_W12_C4 1
+#endif
+constexpr int s1_waves(int ns2, int nb) {
+  return ((KM_S1_W12 && ns2 == 2 && nb == 8) || (KM_S1_W12_C4 && ns2 == 1 && nb == 32)) ? 12 : 8;
+}
 
 constexpr int S1_MAX_WAVES = 12;                // per CU, any geometry (change-list counts)
 // rows per re-scoring batch (one per quad of a wave): 16, or 12 where twelve
@@ -931,7 +936,7 @@ __global__ __launch_bounds__(s1_waves(NS2, NB) * 64, s1_waves(NS2, NB) / 4) void
   // this wave's steps gw, gw + nw, ... of TT tiles each; NBUF register
   // buffers of rows: NBUF - 1 steps' loads in flight while one is processed
   // (loads past the end read row n - 1 and are never used)
-  constexpr int NBUF = KM_S1_NBUF > 0 ? KM_S1_NBUF : (NS2 == 1 && NB > 8 ? 3 : 2);
+  constexpr int NBUF = KM_S1_NBUF > 0 ? KM_S1_NBUF : (NS2 == 1 && NB > 8 && S1_WAVES == 8 ? 3 : 2);
   const uint32_t nst = (ntiles + (uint32_t)TT - 1u) / (uint32_t)TT;
   Buf b[NBUF][TT];
   auto load_step = [&](uint32_t st, Buf (&BB)[TT]) {
