@@ -123,7 +123,7 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
                               int32_t* labels, QEntry* queue, uint32_t* qcount, int n_cu, QLayout* ql,
                               const int* gate, hipStream_t s, uint32_t* cand = nullptr, uint32_t* cand_ctr = nullptr,
                               uint32_t cand_cap = 0, int one = 0,
-                              const float* C32 = nullptr);
+                              const float* C32 = nullptr, uint2* chg = nullptr, uint32_t* chg_cnt = nullptr);
 int cand_rec_words();
 // queue capacity (entries) and per-wave counter words needed for n rows
 size_t queue_capacity(int64_t n, int n_cu);
@@ -251,6 +251,10 @@ bool s1_delta_ok(const Geometry& g, int n_cu);
 // delta statistics: the change list of k_s1 into stats (deltas)
 hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt,
                            double* stats, int n_cu, const int* gate, hipStream_t s);
+// the same for any change list of nw wave segments of seg entries
+// (k_assign_mfma16's delta mode: its queue layout)
+hipError_t launch_chg_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt, int nw,
+                            uint32_t seg, double* stats, int n_cu, const int* gate, hipStream_t s);
 // delta statistics: mode 1 full += stats, stats = full; mode 0 full = stats
 hipError_t launch_s1_apply(double* stats, double* full, int64_t len, int mode, const int* gate, hipStream_t s);
 hipError_t launch_gen_blobs(float* X, const Geometry& g, int64_t row_offset, int32_t n_centers, float box,

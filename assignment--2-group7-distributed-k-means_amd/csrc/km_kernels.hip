@@ -851,6 +851,12 @@ struct MfmaArgs {
   uint32_t cand_cap;   // records
   int one = 0;         // k_assign_mfma16: one fp16 MFMA per product (KM_SCREEN_ONE)
   const float* C32 = nullptr;  // ONE: fp32 centroids [kp][dp], the in-kernel pair re-score
+  // delta statistics (k_assign_mfma16): the previous labels are read; a
+  // decided row whose label changed is written and appended to its wave's
+  // change-list segment {row, old << 16 | new} ([wave][seg], count in
+  // chg_cnt[wave]); queued rows keep their previous label for the resolvers
+  uint2* chg = nullptr;
+  uint32_t* chg_cnt = nullptr;
 };
 
 // LDS image of a centroid chunk: for block b (32 centroids) and K-step t the
@@ -1410,7 +1416,8 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
 
   const uint32_t gw = blockIdx.x * WAVES + wave;
   QEntry* wq = A.queue + (size_t)gw * A.seg;
-  uint32_t qn = 0, qf = 0;
+  uint32_t qn = 0, qf = 0, cc = 0;
+  uint2* wc = A.chg != nullptr ? A.chg + (size_t)gw * A.seg : nullptr;
   const char* laneHi = sHi + lane * 16;
   const char* laneLo = sLo + lane * 16;
   const float* laneCn = sCn + 4 * q;
@@ -1425,6 +1432,8 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
     if (nchunks == 1 && tile >= ntiles) break;  // no barriers below in this mode
     const int64_t row = tile * 32 + prow;       // the row this lane owns after the merge
     const bool valid = row < n;
+    // delta statistics: the row's previous label, loaded now (used at the end)
+    const int32_t old_raw = (wc != nullptr && valid) ? A.labels[row] : 0;
 
     // B operands: lane l holds features 32 sl + 8 q .. + 8 of rows 16 pg + (l & 15)
     f16x8 bh[2][NS2], bl[2][NS2];
@@ -1803,7 +1812,23 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
     }
     const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
     const bool lead = (q & 1) == 0;  // one lane of each pair (l, l ^ 16) writes
-    if (lead && valid) A.labels[row] = lab;
+    if (wc == nullptr) {
+      if (lead && valid) A.labels[row] = lab;
+    } else {
+      // decided rows whose label changed: written and listed; queued rows keep
+      // their previous label (the resolvers compare and move them)
+      const int old = (int)min((uint32_t)old_raw, (uint32_t)(A.k - 1));
+      const bool changed = lead && valid && kind == 0u && lab != old;
+      const uint64_t mc = __ballot(changed);
+      if (mc) {
+        if (changed) {
+          A.labels[row] = lab;
+          wc[cc + (uint32_t)__popcll(mc & ((1ull << lane) - 1ull))] =
+              make_uint2((uint32_t)row, ((uint32_t)old << 16) | (uint32_t)lab);
+        }
+        cc += (uint32_t)__popcll(mc);
+      }
+    }
     const bool enq = lead && valid && (kind != 0);
     const uint64_t m = __ballot(enq);
     if (m) {
@@ -1827,6 +1852,7 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
   if (lane == 0) {
     A.qcount[2 * gw] = qn;
     A.qcount[2 * gw + 1] = qf;
+    if (A.chg_cnt != nullptr) A.chg_cnt[gw] = cc;
   }
 }
 
@@ -2205,7 +2231,7 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
                               const float* cn2s, const float* cmax, const float* xabs, const float* cabs,
                               int32_t* labels, QEntry* queue, uint32_t* qcount, int n_cu, QLayout* ql,
                               const int* gate, hipStream_t s, uint32_t* cand, uint32_t* cand_ctr,
-                              uint32_t cand_cap, int one, const float* C32) {
+                              uint32_t cand_cap, int one, const float* C32, uint2* chg, uint32_t* chg_cnt) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
@@ -2242,8 +2268,11 @@ hipError_t launch_assign_mfma(const float* X, const Geometry& g, const _Float16*
     const hipError_t e = hipMemsetAsync(cand_ctr, 0, sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
   }
+  const bool mfma16 = g.dp % 32 == 0 && g.dp <= 128 && KM_MFMA16;
+  if (chg != nullptr && !mfma16) return hipErrorInvalidValue;  // delta statistics: k_assign_mfma16 only
   MfmaArgs a{X, g.n, g.k, g.kp, KC, seg, Chi, Clo, cn2s, cmax, xabs, cabs, labels, queue, qcount, gate,
-             use_cand ? cand : nullptr, cand_ctr, cand_cap, (one && g.dp % 32 == 0 && g.dp <= 256) ? 1 : 0, C32};
+             use_cand ? cand : nullptr, cand_ctr, cand_cap, (one && g.dp % 32 == 0 && g.dp <= 256) ? 1 : 0, C32,
+             chg, chg_cnt};
   switch (g.dp / 16) {
     case 1: launch_mfma_ns<1>(waves, nb, lds, s, a); break;
     case 2: launch_mfma_ns<2>(waves, nb, lds, s, a); break;

@@ -94,6 +94,12 @@ struct km_ctx {
   // The choice depends only on the call sequence, never on a rank's data, so
   // every rank of a job takes the same one.
   bool s1 = false;
+  // delta statistics on the unfused k_assign_mfma16 geometries as well (c5
+  // class: dp a multiple of 32 up to 128): its delta mode writes a change
+  // list in its queue layout (chg_m), folded like k_s1's
+  bool mdelta_geo = false;
+  uint2* chg_m = nullptr;        // k_assign_mfma16 change list [wave][seg] (queue capacity)
+  uint32_t* chg_m_cnt = nullptr; // entries per wave
   bool s1_recolor = true;        // colour the chains at the next prep
   int32_t* s1_perm = nullptr;    // table index -> centroid
   float* s1_cft = nullptr;       // fp32 centroids by table index (LDS copy)
@@ -289,6 +295,7 @@ void free_centroids(km_ctx* c) {
   dfree(c->chg);
   dfree(c->chg_cnt);
   c->s1 = false;
+  c->mdelta_geo = false;
   c->delta_ready = false;
   c->stats_pending = 0;
   dfree(c->work);
@@ -320,6 +327,8 @@ void free_data(km_ctx* c) {
   dfree(c->cand);
   dfree(c->cand_ctr);
   c->cand_cap = 0;
+  dfree(c->chg_m);
+  dfree(c->chg_m_cnt);
   dfree(c->moments);
   dfree(c->xabs);
   dfree(c->xnorm);
@@ -499,7 +508,7 @@ int apply_stats(km_ctx* c, const double** upd_src = nullptr, bool clear = false)
   const int kind = c->stats_pending;
   c->stats_pending = 0;
   if (upd_src) *upd_src = c->stats;
-  if (!c->s1) return KM_OK;
+  if (!c->s1 && !c->mdelta_geo) return KM_OK;
   // full sums (kind 1) become the base of the next deltas, the deltas
   // (kind 2) are folded into them (k_s1_apply replaces the SSE slot)
   const bool keep = kind == 2 || kind == 1;
@@ -646,16 +655,34 @@ int run_assign(km_ctx* c, bool with_stats) {
     const int rc = ensure_x3(c);
     if (rc != KM_OK) return rc;
   }
+  // delta statistics (c5 class, no SSE): the screen lists the rows whose
+  // label changed, the resolvers move their changed rows, and the change list
+  // is folded into the deltas -- no statistics pass over X
+  const bool mdelta = with_stats && c->mdelta_geo && c->delta_ready && !c->want_sse && !c->stats_exported;
+  if (mdelta && !c->chg_m) {
+    KM_HIP(hipMalloc(&c->chg_m, sizeof(uint2) * km::queue_capacity(std::max<int64_t>(g.n, 1), c->n_cu)));
+    KM_HIP(hipMalloc(&c->chg_m_cnt, sizeof(uint32_t) * km::qcount_words(c->n_cu)));
+  }
   {
     ProfScope ps(c, KM_K_ASSIGN);
     KM_HIP(km::launch_assign_mfma(c->X, g, c->Chi, c->Clo, c->cn2s, c->cmax, c->xabs, c->cabs, c->labels, c->queue,
                                   c->qcount, c->n_cu, &c->ql, c->gate, c->stream, c->cand, c->cand_ctr,
-                                  c->cand_cap, one_screen(c) ? 1 : 0, KM_PAIR_RESCORE ? c->C32 : nullptr));
+                                  c->cand_cap, one_screen(c) ? 1 : 0, KM_PAIR_RESCORE ? c->C32 : nullptr,
+                                  mdelta ? c->chg_m : nullptr, mdelta ? c->chg_m_cnt : nullptr));
   }
   {
     ProfScope ps(c, KM_K_RESOLVE);
-    KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels, nullptr, c->n_cu,
-                              c->gate, c->stream, nullptr, c->cand, c->cand_cap));
+    KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels,
+                              mdelta ? c->stats : nullptr, c->n_cu, c->gate, c->stream, nullptr, c->cand, c->cand_cap,
+                              mdelta ? 1 : 0));
+  }
+  if (mdelta) {
+    ProfScope ps(c, KM_K_STATS);
+    KM_HIP(km::launch_chg_delta(c->X, g, c->chg_m, c->chg_m_cnt, (int)c->ql.nwaves, c->ql.seg, c->stats, c->n_cu,
+                                c->gate, c->stream));
+    c->stats_pending = 2;
+    c->last_delta = true;
+    return KM_OK;
   }
   }
   if (with_stats) {
@@ -984,6 +1011,9 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
     // of the unfused screen (c4 class: labels, then the statistics pass)
     c->s1 = (c->path == 2) && (!c->fused || km::fused16_ok(c->g)) && km::s1_ok(c->g) &&
             km::diag_env("KM_S1", 1) != 0;
+    c->mdelta_geo = (c->path == 2) && !c->fused && !c->s1 && c->g.dp % 32 == 0 && c->g.dp <= 128 &&
+                    c->g.k <= 65535 && km::diag_env("KM_MDELTA", 1) != 0;
+    if (c->mdelta_geo) KM_HIP(hipMalloc(&c->stats_full, sizeof(double) * stats_len(c->g)));
     if (c->s1) {
       const size_t nt = km::s1_table_entries(c->g);
       KM_HIP(hipMalloc(&c->s1_perm, sizeof(int32_t) * nt));

@@ -1130,6 +1130,25 @@ bool s1_delta_ok(const Geometry& g, int n_cu) {
   return g.k <= 65535;
 }
 
+hipError_t launch_chg_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt, int nw,
+                            uint32_t seg, double* stats, int n_cu, const int* gate, hipStream_t s) {
+  if (g.n == 0 || nw == 0) return hipSuccess;
+  if (g.k > 65535) return hipErrorInvalidValue;
+  const size_t pre = ((size_t)nw + 1) * 4;
+  if (pre > 64 * 1024) return hipErrorInvalidValue;
+  // the LDS aggregation where the table fits beside the largest k_s1 grid's
+  // prefix (a choice by geometry only: s1_delta_lds_ok), else direct atomics
+  const size_t tab = (size_t)g.k * (g.d + 1) * 8;
+  if (s1_ok(g) ? s1_delta_lds_ok(g, n_cu) : tab + pre <= 160 * 1024) {
+    hipLaunchKernelGGL(k_s1_delta<false>, dim3(n_cu), dim3(1024), tab + pre, s, X, g.dp, g.d, g.k, chg, chg_cnt, nw,
+                       seg, stats, gate);
+  } else {
+    hipLaunchKernelGGL(k_s1_delta<true>, dim3(n_cu), dim3(1024), pre, s, X, g.dp, g.d, g.k, chg, chg_cnt, nw, seg,
+                       stats, gate);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt,
                            double* stats, int n_cu, const int* gate, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
@@ -1137,15 +1156,7 @@ hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, 
   uint32_t seg;
   const int64_t nw = s1_grid(g, n_cu, &nbk, &seg);
   if (!s1_delta_ok(g, n_cu)) return hipErrorInvalidValue;
-  if (s1_delta_lds_ok(g, n_cu)) {
-    const size_t lds = s1_delta_lds(g, n_cu);  // (nw <= n_cu * waves)
-    hipLaunchKernelGGL(k_s1_delta<false>, dim3(n_cu), dim3(1024), lds, s, X, g.dp, g.d, g.k, chg, chg_cnt, (int)nw,
-                       seg, stats, gate);
-  } else {
-    hipLaunchKernelGGL(k_s1_delta<true>, dim3(n_cu), dim3(1024), ((size_t)nw + 1) * 4, s, X, g.dp, g.d, g.k, chg,
-                       chg_cnt, (int)nw, seg, stats, gate);
-  }
-  return hipGetLastError();
+  return launch_chg_delta(X, g, chg, chg_cnt, (int)nw, seg, stats, n_cu, gate, s);
 }
 
 hipError_t launch_s1_apply(double* stats, double* full, int64_t len, int mode, const int* gate, hipStream_t s) {

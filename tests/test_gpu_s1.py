@@ -506,3 +506,40 @@ def test_one_mfma_unfused_screen_fit_c5_shape():
     ref = orc.lloyd_fit(X, 4096, 3, 1e-12, 0, True, 1, init_centroids=C0, empty_seed=lambda: SEED)
     np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
     np.testing.assert_allclose(km.sse_history, ref["sse_history"], rtol=1e-9)
+
+
+@pytest.mark.parametrize("n,d,k,centers,iters", [
+    (12000, 128, 4096, 1024, 4),  # c5 geometry: chunked images, one-MFMA screen, direct-atomic deltas
+    (12000, 64, 1536, 300, 5),    # dp 64, kp 1536 (no k_s1 instance): the same screen and deltas
+])
+def test_one_mfma_unfused_screen_delta_statistics(n, d, k, centers, iters):
+    # the unfused k_assign_mfma16 geometries take delta statistics too (round
+    # 6, compute_sse off): from the second iteration the screen lists the rows
+    # whose label changed, the resolvers move their changed rows, and
+    # k_s1_delta folds the list -- no statistics pass over X
+    X = _blobs(n, d, centers, seed=83 + d)
+    C0 = X[np.random.default_rng(84).choice(len(X), k, replace=False)]
+    km = _fit(X, C0, iters)
+    eng = km._runner.engine
+    assert eng.screen() == ONE and eng.info()["delta_stats"] == 1
+    ref = orc.lloyd_fit(X, k, iters, 1e-12, 0, False, 1, init_centroids=C0, empty_seed=lambda: SEED)
+    np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
+    C_prev = orc.lloyd_fit(X, k, iters - 1, 1e-12, 0, False, 1, init_centroids=C0, empty_seed=lambda: SEED)["centroids"]
+    np.testing.assert_array_equal(eng.labels(), orc.assign(X, C_prev)[0])
+    np.testing.assert_array_equal(km._runner.last["counts"], np.bincount(eng.labels(), minlength=k))
+
+
+def test_one_mfma_unfused_poor_seeds_delta_statistics():
+    # c5's poor seeds (3 data rows + far points: mass empties repaired on the
+    # device at iteration 1), then delta iterations over the repaired
+    # centroids, against the oracle's whole loop (pinned repair seed)
+    n, d, k = 12000, 128, 1024
+    X = _blobs(n, d, 64, seed=57)
+    far = np.full((k - 3, d), 100.0) + np.arange(k - 3)[:, None]
+    C0 = np.vstack([X[[0, 1, 2]], far])
+    km = _fit(X, C0, 4)
+    eng = km._runner.engine
+    assert eng.info()["delta_stats"] == 1 and km._runner.device_repairs >= 1
+    ref = orc.lloyd_fit(X, k, 4, 1e-12, 0, False, 1, init_centroids=C0, empty_seed=lambda: SEED)
+    assert ref["records"][0]["empty"]
+    np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
