@@ -101,6 +101,8 @@ struct km_ctx {
   uint2* chg_m = nullptr;        // k_assign_mfma16 change list [wave][seg] (queue capacity)
   uint32_t* chg_m_cnt = nullptr; // entries per wave
   bool s1_recolor = true;        // colour the chains at the next prep
+  int s1_color_age = 0;          // batches since the last colouring
+  int s1_batches = 0;            // batches since new centroids
   int32_t* s1_perm = nullptr;    // table index -> centroid
   float* s1_cft = nullptr;       // fp32 centroids by table index (LDS copy)
   float* s1_cn2o = nullptr;      // s^2 ||c||^2, MFMA output order
@@ -1027,6 +1029,8 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
     }
   }
   c->s1_recolor = true;
+  c->s1_color_age = 0;
+  c->s1_batches = 0;
   c->delta_ready = false;
   c->stats_pending = 0;
   KM_HIP(hipMemcpyAsync(c->C64_cur, C, sizeof(double) * k * d, hipMemcpyHostToDevice, c->stream));
@@ -1212,10 +1216,15 @@ int km_batch_begin(km_ctx* c) {
   KM_REQUIRE(!c->in_batch, KM_ERR_STATE, "km_batch_begin: a batch is open");
   KM_HIP(hipSetDevice(c->device));
   KM_HIP(hipMemsetAsync(c->gate, 0, sizeof(int), c->stream));
-  if (c->s1) {
-    // the chain colouring follows the centroids once per batch (a stale one
-    // only queues rows: the certificate uses R_c of the current centroids)
+  if (c->s1 && (++c->s1_batches <= 3 || ++c->s1_color_age >= 4)) {
+    // the chain colouring follows the centroids at each of the first three
+    // batches after new centroids (4 + 8 + 16 iterations, while they move
+    // most), then every fourth batch (batches grow to 32 iterations; one
+    // colouring is a sequential pass over k, ~0.8 ms at k = 256).  A stale
+    // colouring can only queue rows, never mislabel them (the certificate
+    // holds for any colouring: km_screen1.hip k_s1_color)
     c->s1_recolor = true;
+    c->s1_color_age = 0;
     if (c->prep_of == c->C64_cur) c->prep_of = nullptr;
   }
   c->in_batch = true;
