@@ -130,13 +130,16 @@ size_t queue_capacity(int64_t n, int n_cu);
 size_t qcount_words(int n_cu);
 bool mfma_path_ok(const Geometry& g);
 // stats != nullptr: also add the resolved points' rows to the partial sums
-// delta: the queued rows still hold their previous labels (k_s1 delta mode);
-// a resolved row whose label changed moves its x between the sums in stats
+// delta: the queued rows still hold their previous labels (delta statistics);
+// each resolved row writes {row, old << 16 | new} into the change list chg of
+// the screen, behind the screen's chg_cnt[w] entries of its wave segment w
+// (re-rank entries first, then full scans: chg_cnt[w] + qcount[2w] +
+// qcount[2w+1] <= seg entries), stats unused; launch_chg_delta folds them
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
                           double* stats, int n_cu, const int* gate, hipStream_t s, double* sse = nullptr,
                           const uint32_t* cand = nullptr, uint32_t cand_cap = 0, int delta = 0,
-                          const float* sse_c32 = nullptr);
+                          const float* sse_c32 = nullptr, uint2* chg = nullptr, const uint32_t* chg_cnt = nullptr);
 // Fused assign + partial sums (kp*dp <= 16384 class): fp16 hi image in VGPRs,
 // lo image + float64 sum table in LDS; decided points summed here, queued
 // points (and their counts) by launch_resolve(stats).
@@ -250,11 +253,13 @@ size_t s1_wave_slots(int n_cu);
 bool s1_delta_ok(const Geometry& g, int n_cu);
 // delta statistics: the change list of k_s1 into stats (deltas)
 hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt,
-                           double* stats, int n_cu, const int* gate, hipStream_t s);
+                           double* stats, int n_cu, const int* gate, hipStream_t s, const uint32_t* qcount = nullptr);
 // the same for any change list of nw wave segments of seg entries
-// (k_assign_mfma16's delta mode: its queue layout)
+// (k_assign_mfma16's delta mode: its queue layout); qcount != nullptr: each
+// segment also holds the resolvers' entries (launch_resolve with delta)
 hipError_t launch_chg_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt, int nw,
-                            uint32_t seg, double* stats, int n_cu, const int* gate, hipStream_t s);
+                            uint32_t seg, double* stats, int n_cu, const int* gate, hipStream_t s,
+                            const uint32_t* qcount = nullptr);
 // delta statistics: mode 1 full += stats, stats = full; mode 0 full = stats
 hipError_t launch_s1_apply(double* stats, double* full, int64_t len, int mode, const int* gate, hipStream_t s);
 hipError_t launch_gen_blobs(float* X, const Geometry& g, int64_t row_offset, int32_t n_centers, float box,

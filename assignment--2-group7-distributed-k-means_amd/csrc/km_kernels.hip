@@ -3707,7 +3707,8 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
                                                   int32_t* __restrict__ labels, double* __restrict__ stats,
                                                   int tab_kp, double* __restrict__ sse, const int* __restrict__ gate,
                                                   const uint32_t* __restrict__ cand, uint32_t cand_cap, int delta,
-                                                  const float* __restrict__ sse_c32) {
+                                                  const float* __restrict__ sse_c32, uint2* __restrict__ chg,
+                                                  const uint32_t* __restrict__ chg_cnt) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* tab = reinterpret_cast<double*>(smem);
@@ -3726,9 +3727,11 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
        g += ng) {
     const bool have = g < total;
     QEntry q{0, 0, 0, 0};
+    size_t cpos = 0;  // delta: this entry's slot in the change list
     if (have) {
       const uint32_t sg = find_segment(pre, ql.nwaves, g);
       q = queue[(size_t)sg * ql.seg + (g - pre[sg])];
+      if (delta) cpos = (size_t)sg * ql.seg + chg_cnt[sg] + (g - pre[sg]);
     }
     // kind 4: a candidate list (k_assign_mfma), count + ascending indices
     const uint32_t* rec = (have && q.kind == 4u && cand != nullptr && q.i2 < cand_cap)
@@ -3808,17 +3811,10 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
       const double mn = ok ? mnorm : rsq_bad;
       ss_acc += mn * mn;
     }
-    if (stats && delta) {
-      if (old != lab) {  // the row moves from cluster old to lab
-        for (int f = u; f < d; f += 8) {
-          atomicAdd(stats + (size_t)old * (d + 1) + f, -(double)x[f]);
-          atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)x[f]);
-        }
-        if (u == 0) {
-          atomicAdd(stats + (size_t)old * (d + 1) + d, -1.0);
-          atomicAdd(stats + (size_t)lab * (d + 1) + d, 1.0);
-        }
-      }
+    if (delta) {
+      // the row's entry behind the screen's changes in its wave segment
+      // (old == lab: no move), folded with them by k_s1_delta
+      if (u == 0) chg[cpos] = make_uint2(q.row, ((uint32_t)old << 16) | (uint32_t)lab);
     } else if (stats) {
       for (int f = u; f < d; f += 8) {
         if (tab_kp)
@@ -3890,7 +3886,8 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
                                                    int32_t* __restrict__ labels, int ch,
                                                    double* __restrict__ stats, int use_chain, int pair_chain,
                                                    double* __restrict__ sse, const int* __restrict__ gate, int delta,
-                                                   const float* __restrict__ sse_c32) {
+                                                   const float* __restrict__ sse_c32, uint2* __restrict__ chg,
+                                                   const uint32_t* __restrict__ chg_cnt) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sCT = reinterpret_cast<double*>(smem);                                    // [d][ch]
@@ -3910,6 +3907,7 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
     // the G entries' queue words, then their rows, each as one batch of
     // independent loads (past-the-end slots read the last entry, unused)
     QEntry qe[G];
+    size_t cpos[G];  // delta: the entries' slots in the change list
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const uint32_t e = b0 + (uint32_t)(wave * G + g);
@@ -3917,6 +3915,7 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
       const uint32_t ec = have[g] ? e : total - 1u;
       const uint32_t sg = find_segment(pre, ql.nwaves, ec);
       qe[g] = queue[(size_t)sg * ql.seg + (ql.seg - 1u - (ec - pre[sg]))];
+      cpos[g] = delta ? (size_t)sg * ql.seg + chg_cnt[sg] + qcount[2 * sg] + (ec - pre[sg]) : 0;
     }
     float xv[G][4];  // features [0, 256); wider rows stage the rest below
 #pragma unroll
@@ -3969,17 +3968,10 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
       } else if (sse && lane == 0 && bi >= 0) {
         ss_acc += bv * bv;  // min_distance ** 2 (bv: the norm)
       }
-      if (stats && delta) {
-        if (old != lab) {  // the row moves from cluster old to lab
-          for (int f = lane; f < d; f += 64) {
-            atomicAdd(stats + (size_t)old * (d + 1) + f, -(double)xs[g * d + f]);
-            atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)xs[g * d + f]);
-          }
-          if (lane == 0) {
-            atomicAdd(stats + (size_t)old * (d + 1) + d, -1.0);
-            atomicAdd(stats + (size_t)lab * (d + 1) + d, 1.0);
-          }
-        }
+      if (delta) {
+        // the row's entry behind the screen's changes and the re-rank
+        // entries of its wave segment (old == lab: no move; k_s1_delta)
+        if (lane == 0) chg[cpos[g]] = make_uint2(rows[g], ((uint32_t)old << 16) | (uint32_t)lab);
       } else if (stats) {
         for (int f = lane; f < d; f += 64) atomicAdd(stats + (size_t)lab * (d + 1) + f, (double)xs[g * d + f]);
         if (lane == 0) atomicAdd(stats + (size_t)lab * (d + 1) + d, 1.0);  // count
@@ -4124,8 +4116,11 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
                           double* stats, int n_cu, const int* gate, hipStream_t s, double* sse,
-                          const uint32_t* cand, uint32_t cand_cap, int delta, const float* sse_c32) {
+                          const uint32_t* cand, uint32_t cand_cap, int delta, const float* sse_c32, uint2* chg,
+                          const uint32_t* chg_cnt) {
   if (g.n == 0 || ql.nwaves == 0) return hipSuccess;
+  if (delta && (!chg || !chg_cnt || g.k > 65535)) return hipErrorInvalidValue;
+  if (delta) stats = nullptr;  // the moves go to the change list
   constexpr size_t LDS_MAX = 160 * 1024;
   const size_t pre_bytes = ((size_t)ql.nwaves + 1) * 4;
   if (pre_bytes > LDS_MAX / 4) return hipErrorInvalidValue;
@@ -4144,16 +4139,16 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   static const int fs_wg = diag_env("KM_FS_WG", 1);  // workgroups per CU (3: no measurable change)
   if (ch == 0)
     hipLaunchKernelGGL((k_fullscan<2, true>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
-                       queue, qcount, ql, labels, ch, delta ? stats : (double*)nullptr, use_chain, pair_chain, sse, gate,
-                       delta, sse_c32);
+                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, sse, gate, delta, sse_c32, chg,
+                       chg_cnt);
   else if (G == 4)
     hipLaunchKernelGGL((k_fullscan<4, false>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
-                       queue, qcount, ql, labels, ch, delta ? stats : (double*)nullptr, use_chain, pair_chain, sse, gate,
-                       delta, sse_c32);
+                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, sse, gate, delta, sse_c32, chg,
+                       chg_cnt);
   else
     hipLaunchKernelGGL((k_fullscan<2, false>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
-                       queue, qcount, ql, labels, ch, delta ? stats : (double*)nullptr, use_chain, pair_chain, sse, gate,
-                       delta, sse_c32);
+                       queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, sse, gate, delta, sse_c32, chg,
+                       chg_cnt);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t tab_bytes = (size_t)(g.d + 1) * g.kp * 8;
@@ -4168,10 +4163,12 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   const int rwg = std::max(1, n_cu * std::max(1, rpct) / 100);
   if (g.d > 256)
     hipLaunchKernelGGL(k_rerank2<true>, dim3(rwg), dim3(512), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
-                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap, delta, sse_c32);
+                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap, delta, sse_c32, chg,
+                       chg_cnt);
   else
     hipLaunchKernelGGL(k_rerank2<false>, dim3(rwg), dim3(1024), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
-                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap, delta, sse_c32);
+                       g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap, delta, sse_c32, chg,
+                       chg_cnt);
   return hipGetLastError();
 }
 

@@ -590,14 +590,14 @@ int run_assign(km_ctx* c, bool with_stats) {
       // the chain certificate leaves open, resolved in float64 (delta: they
       // still hold their previous labels)
       ProfScope ps(c, KM_K_RESOLVE);
-      KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels,
-                                with_stats ? c->stats : nullptr, c->n_cu, c->gate, c->stream, s1_sse, nullptr, 0,
-                                with_stats ? 1 : 0, s1_sse ? c->C32 : nullptr));
+      KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels, nullptr,
+                                c->n_cu, c->gate, c->stream, s1_sse, nullptr, 0, with_stats ? 1 : 0,
+                                s1_sse ? c->C32 : nullptr, c->chg, c->chg_cnt));
     }
     if (with_stats) {
       // the rows k_s1 moved between clusters (its change list) into the deltas
       ProfScope ps(c, KM_K_STATS);
-      KM_HIP(km::launch_s1_delta(c->X, g, c->chg, c->chg_cnt, c->stats, c->n_cu, c->gate, c->stream));
+      KM_HIP(km::launch_s1_delta(c->X, g, c->chg, c->chg_cnt, c->stats, c->n_cu, c->gate, c->stream, c->qcount));
     }
     if (with_stats) {
       c->stats_pending = 2;
@@ -674,14 +674,14 @@ int run_assign(km_ctx* c, bool with_stats) {
   }
   {
     ProfScope ps(c, KM_K_RESOLVE);
-    KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels,
-                              mdelta ? c->stats : nullptr, c->n_cu, c->gate, c->stream, nullptr, c->cand, c->cand_cap,
-                              mdelta ? 1 : 0));
+    KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels, nullptr, c->n_cu,
+                              c->gate, c->stream, nullptr, c->cand, c->cand_cap, mdelta ? 1 : 0, nullptr,
+                              mdelta ? c->chg_m : nullptr, mdelta ? c->chg_m_cnt : nullptr));
   }
   if (mdelta) {
     ProfScope ps(c, KM_K_STATS);
     KM_HIP(km::launch_chg_delta(c->X, g, c->chg_m, c->chg_m_cnt, (int)c->ql.nwaves, c->ql.seg, c->stats, c->n_cu,
-                                c->gate, c->stream));
+                                c->gate, c->stream, c->qcount));
     c->stats_pending = 2;
     c->last_delta = true;
     return KM_OK;

@@ -990,37 +990,48 @@ __global__ __launch_bounds__(256) void k_s1_apply(double* __restrict__ stats, do
   stats[i] = mode == 2 ? 0.0 : v;
 }
 
-// The change list of k_s1 into the delta statistics.  The list is nw wave
-// segments of seg entries, cnt[w] used in segment w; every workgroup scans
-// the counts (exclusive prefix in LDS), takes a contiguous slice of the
-// concatenated list (at least S1D_MIN entries, so a short list wakes few
-// workgroups and flushes few tables), moves each changed row's x from its
-// old cluster to its new one in an LDS float64 table [k][d+1] (lanes over
-// features: consecutive banks), 8 rows per wave in flight, then adds the
-// table's non-zero entries to the statistics with global atomics.
+// A change list into the delta statistics.  The list is nw wave segments
+// of seg entries {row, old << 16 | new}: segment w holds cnt[w] entries of
+// the screen and, with qcount (delta resolvers, launch_resolve), qcount[2w] +
+// qcount[2w+1] entries of the resolvers behind them (old == new: the row kept
+// its label, skipped without reading it).  The clusters are split into
+// `nr` ranges of kr, each small enough for an LDS float64 table [kr][d+1];
+// workgroup b aggregates range b % nr over slice b / nr of the concatenated
+// list (at least S1D_MIN entries, so a short list wakes few workgroups): each
+// wave takes 64 entries at a time (one per lane, its segment by a binary
+// search of the LDS prefix), keeps those with an end in its range (ballot),
+// and moves their rows 8 at a time (lanes over features, the x loads of the
+// 8 issued together) with LDS float64 atomics; the table's non-zero entries
+// then go to the statistics with global atomics.  An entry is read by every
+// range's workgroups (8 B each) but its row only by the workgroups of its two
+// clusters, so no float64 atomic reaches global memory per changed row: the
+// c4 and c5 classes, whose [k][d+1] table exceeds LDS, fold millions of
+// changed rows (poor seeds, first iterations) at the cost of reading them.
 #ifndef KM_S1D_MIN
 #define KM_S1D_MIN 256
 #endif
 constexpr uint32_t S1D_MIN = KM_S1D_MIN;
 constexpr int S1D_ROWS = 8;
-// DIRECT (the table does not fit LDS: c4 class, k (d + 1) doubles > 160 KiB):
-// each changed row goes straight to the statistics with float64 global
-// atomics (few rows change in steady state).
-template <bool DIRECT>
 __global__ __launch_bounds__(1024) void k_s1_delta(const float* __restrict__ X, int dp, int d, int k,
                                                    const uint2* __restrict__ chg, const uint32_t* __restrict__ cnt,
-                                                   int nw, uint32_t seg, double* __restrict__ stats,
+                                                   const uint32_t* __restrict__ qcount, int nw, uint32_t seg, int kr,
+                                                   int nr, double* __restrict__ stats,
                                                    const int* __restrict__ gate) {
   if (*gate) return;
-  extern __shared__ double smem_d[];  // [k][d + 1] (not DIRECT), then pre[nw + 1]
+  extern __shared__ double smem_d[];  // [kr][d + 1], then pre[nw + 1]
   const int d1 = d + 1;
-  double* tab = DIRECT ? stats : smem_d;
-  uint32_t* pre = reinterpret_cast<uint32_t*>(smem_d + (DIRECT ? 0 : (size_t)k * d1));
+  double* tab = smem_d;
+  uint32_t* pre = reinterpret_cast<uint32_t*>(smem_d + (size_t)kr * d1);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   if (wave == 0) {
     uint32_t run = 0;
     for (int b = 0; b < nw; b += 64) {
-      const uint32_t v = b + lane < nw ? cnt[b + lane] : 0u;
+      uint32_t v = 0;
+      if (b + lane < nw) {
+        v = cnt[b + lane];
+        if (qcount) v += qcount[2 * (b + lane)] + qcount[2 * (b + lane) + 1];
+        v = min(v, seg);
+      }
       uint32_t inc = v;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
@@ -1033,57 +1044,77 @@ __global__ __launch_bounds__(1024) void k_s1_delta(const float* __restrict__ X, 
     if (lane == 0) pre[nw] = run;
   }
   __syncthreads();
+  const int r = (int)(blockIdx.x % (uint32_t)nr);
+  const uint32_t ns = gridDim.x / (uint32_t)nr, sl = blockIdx.x / (uint32_t)nr;
   const uint32_t nc = pre[nw];
-  const uint32_t per = max(S1D_MIN, (nc + gridDim.x - 1u) / gridDim.x);
-  const uint32_t e0 = blockIdx.x * per;
-  if (e0 >= nc) return;
+  const uint32_t per = max(S1D_MIN, (nc + ns - 1u) / ns);
+  const uint32_t e0 = sl * per;
+  if (sl >= ns || e0 >= nc) return;
   const uint32_t e1 = min(nc, e0 + per);
-  if constexpr (!DIRECT)
-    for (int i = threadIdx.x; i < k * d1; i += blockDim.x) tab[i] = 0.0;
+  const uint32_t lo = (uint32_t)r * (uint32_t)kr;
+  const uint32_t span = min((uint32_t)kr, (uint32_t)k - lo);
+  for (int i = threadIdx.x; i < (int)span * d1; i += blockDim.x) tab[i] = 0.0;
   __syncthreads();
   // entry e of the concatenation: segment w = the last with pre[w] <= e
   auto at = [&](uint32_t e) {
-    int lo = 0, hi = nw - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (pre[mid] <= e) lo = mid; else hi = mid - 1;
+    int a = 0, h = nw - 1;
+    while (a < h) {
+      const int mid = (a + h + 1) >> 1;
+      if (pre[mid] <= e) a = mid; else h = mid - 1;
     }
-    return chg[(size_t)lo * seg + (e - pre[lo])];
+    return chg[(size_t)a * seg + (e - pre[a])];
   };
-  for (uint32_t e = e0 + (uint32_t)wave * S1D_ROWS; e < e1; e += (uint32_t)nwv * S1D_ROWS) {
-    // lanes 0..7 locate the wave's 8 entries, then every lane takes them
-    uint2 mine = make_uint2(0u, 0u);
-    if (lane < S1D_ROWS) mine = at(min(e + (uint32_t)lane, e1 - 1u));
-    uint2 c[S1D_ROWS];
+  for (uint32_t base = e0 + (uint32_t)wave * 64u; base < e1; base += (uint32_t)nwv * 64u) {
+    const uint32_t e = base + (uint32_t)lane;
+    const uint2 c = e < e1 ? at(e) : make_uint2(0u, 0u);
+    const uint32_t o = c.y >> 16, nn = c.y & 0xFFFFu;
+    const bool mine = e < e1 && o != nn && (o - lo < span || nn - lo < span);
+    uint64_t m = __ballot(mine);
+    while (m) {
+      // up to 8 of the wave's entries in range (uniform: m is scalar)
+      uint32_t row[S1D_ROWS], oy[S1D_ROWS];
+      int na = 0;
 #pragma unroll
-    for (int r = 0; r < S1D_ROWS; ++r) c[r] = make_uint2(__shfl(mine.x, r), __shfl(mine.y, r));
-    for (int f0 = 0; f0 < d; f0 += 64) {
-      const int f = f0 + lane;
-      float x[S1D_ROWS];
+      for (int j = 0; j < S1D_ROWS; ++j) {
+        row[j] = 0u;
+        oy[j] = 0u;  // old = new = 0: no move
+        if (m) {
+          const int src = __builtin_ctzll(m);
+          m &= m - 1ull;
+          row[j] = (uint32_t)__builtin_amdgcn_readlane((int)c.x, src);
+          oy[j] = (uint32_t)__builtin_amdgcn_readlane((int)c.y, src);
+          ++na;
+        }
+      }
+      for (int f0 = 0; f0 < d; f0 += 64) {
+        const int f = f0 + lane;
+        float x[S1D_ROWS];
 #pragma unroll
-      for (int r = 0; r < S1D_ROWS; ++r) x[r] = f < d ? X[(size_t)c[r].x * dp + f] : 0.0f;
+        for (int j = 0; j < S1D_ROWS; ++j) x[j] = (j < na && f < d) ? X[(size_t)row[j] * dp + f] : 0.0f;
+        if (f < d)
 #pragma unroll
-      for (int r = 0; r < S1D_ROWS; ++r) {
-        if (e + (uint32_t)r >= e1 || f >= d) continue;
-        const uint32_t old = c[r].y >> 16, nw2 = c[r].y & 0xFFFFu;
-        atomicAdd(tab + (size_t)old * d1 + f, -(double)x[r]);
-        atomicAdd(tab + (size_t)nw2 * d1 + f, (double)x[r]);
+          for (int j = 0; j < S1D_ROWS; ++j) {
+            const uint32_t jo = oy[j] >> 16, jn = oy[j] & 0xFFFFu;
+            if (j >= na) continue;
+            if (jo - lo < span) atomicAdd(tab + (size_t)(jo - lo) * d1 + f, -(double)x[j]);
+            if (jn - lo < span) atomicAdd(tab + (size_t)(jn - lo) * d1 + f, (double)x[j]);
+          }
+      }
+      if (lane < na) {
+        // the counts: lane j takes entry j's two ends
+        uint32_t jy = 0u;
+#pragma unroll
+        for (int j = 0; j < S1D_ROWS; ++j) jy = lane == j ? oy[j] : jy;
+        const uint32_t jo = jy >> 16, jn = jy & 0xFFFFu;
+        if (jo - lo < span) atomicAdd(tab + (size_t)(jo - lo) * d1 + d, -1.0);
+        if (jn - lo < span) atomicAdd(tab + (size_t)(jn - lo) * d1 + d, 1.0);
       }
     }
-    if (lane == 0)
-#pragma unroll
-      for (int r = 0; r < S1D_ROWS; ++r) {
-        if (e + (uint32_t)r >= e1) continue;
-        atomicAdd(tab + (size_t)(c[r].y >> 16) * d1 + d, -1.0);
-        atomicAdd(tab + (size_t)(c[r].y & 0xFFFFu) * d1 + d, 1.0);
-      }
   }
-  if constexpr (!DIRECT) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < k * d1; i += blockDim.x) {
-      const double v = tab[i];
-      if (v != 0.0) atomicAdd(stats + i, v);
-    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < (int)span * d1; i += blockDim.x) {
+    const double v = tab[i];
+    if (v != 0.0) atomicAdd(stats + (size_t)lo * d1 + i, v);
   }
 }
 
@@ -1114,49 +1145,41 @@ size_t s1_chg_entries(const Geometry& g, int n_cu) {
 
 size_t s1_wave_slots(int n_cu) { return (size_t)n_cu * S1_MAX_WAVES; }
 
-// the delta aggregation's LDS table [k][d+1] f64 and the wave-count prefix
-// for the largest grid (n_cu workgroups): geometry and device only, never the
-// rank's row count, so every rank of a job makes the same choice (a rank with
-// few rows has a smaller grid; sizing by its own grid could put it in delta
-// mode while a larger rank sends full sums into the same all-reduce)
-static size_t s1_delta_lds(const Geometry& g, int n_cu) {
-  return (size_t)g.k * (g.d + 1) * 8 + ((size_t)n_cu * s1_geo_waves(g) + 1) * 4;
-}
-// the LDS aggregation fits; otherwise k_s1_delta<DIRECT> (global atomics).
-// Every k_s1 geometry has delta statistics (k < 65536: 16-bit cluster ids)
-static bool s1_delta_lds_ok(const Geometry& g, int n_cu) { return s1_delta_lds(g, n_cu) <= 160 * 1024; }
+// delta statistics on every geometry with 16-bit cluster ids (k_s1_delta
+// splits the clusters into ranges whose LDS tables fit)
 bool s1_delta_ok(const Geometry& g, int n_cu) {
   (void)n_cu;
   return g.k <= 65535;
 }
 
 hipError_t launch_chg_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt, int nw,
-                            uint32_t seg, double* stats, int n_cu, const int* gate, hipStream_t s) {
+                            uint32_t seg, double* stats, int n_cu, const int* gate, hipStream_t s,
+                            const uint32_t* qcount) {
   if (g.n == 0 || nw == 0) return hipSuccess;
   if (g.k > 65535) return hipErrorInvalidValue;
+  constexpr size_t LDS = 160 * 1024;
   const size_t pre = ((size_t)nw + 1) * 4;
-  if (pre > 64 * 1024) return hipErrorInvalidValue;
-  // the LDS aggregation where the table fits beside the largest k_s1 grid's
-  // prefix (a choice by geometry only: s1_delta_lds_ok), else direct atomics
-  const size_t tab = (size_t)g.k * (g.d + 1) * 8;
-  if (s1_ok(g) ? s1_delta_lds_ok(g, n_cu) : tab + pre <= 160 * 1024) {
-    hipLaunchKernelGGL(k_s1_delta<false>, dim3(n_cu), dim3(1024), tab + pre, s, X, g.dp, g.d, g.k, chg, chg_cnt, nw,
-                       seg, stats, gate);
-  } else {
-    hipLaunchKernelGGL(k_s1_delta<true>, dim3(n_cu), dim3(1024), pre, s, X, g.dp, g.d, g.k, chg, chg_cnt, nw, seg,
-                       stats, gate);
-  }
+  const size_t row = (size_t)(g.d + 1) * 8;  // one cluster's table row
+  if (pre > 64 * 1024 || pre + row > LDS) return hipErrorInvalidValue;
+  // ranges of clusters whose [kr][d+1] table fits beside the prefix, as few
+  // as possible, balanced; ~n_cu workgroups (at least one per range)
+  const int kmax = (int)((LDS - pre) / row);
+  const int nr = (g.k + kmax - 1) / kmax;
+  const int kr = (g.k + nr - 1) / nr;
+  const int ns = std::max(1, (n_cu + nr / 2) / nr);
+  hipLaunchKernelGGL(k_s1_delta, dim3((unsigned)(nr * ns)), dim3(1024), (size_t)kr * row + pre, s, X, g.dp, g.d, g.k,
+                     chg, chg_cnt, qcount, nw, seg, kr, nr, stats, gate);
   return hipGetLastError();
 }
 
 hipError_t launch_s1_delta(const float* X, const Geometry& g, const uint2* chg, const uint32_t* chg_cnt,
-                           double* stats, int n_cu, const int* gate, hipStream_t s) {
+                           double* stats, int n_cu, const int* gate, hipStream_t s, const uint32_t* qcount) {
   if (g.n == 0) return hipSuccess;
   int nbk;
   uint32_t seg;
   const int64_t nw = s1_grid(g, n_cu, &nbk, &seg);
   if (!s1_delta_ok(g, n_cu)) return hipErrorInvalidValue;
-  return launch_chg_delta(X, g, chg, chg_cnt, (int)nw, seg, stats, n_cu, gate, s);
+  return launch_chg_delta(X, g, chg, chg_cnt, (int)nw, seg, stats, n_cu, gate, s, qcount);
 }
 
 hipError_t launch_s1_apply(double* stats, double* full, int64_t len, int mode, const int* gate, hipStream_t s) {
