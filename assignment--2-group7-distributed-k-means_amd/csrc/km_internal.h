@@ -135,11 +135,14 @@ bool mfma_path_ok(const Geometry& g);
 // the screen, behind the screen's chg_cnt[w] entries of its wave segment w
 // (re-rank entries first, then full scans: chg_cnt[w] + qcount[2w] +
 // qcount[2w+1] <= seg entries), stats unused; launch_chg_delta folds them
+// C32, cmax (the fp32 images and their largest norm): the full scans run an
+// fp32 prefilter first and evaluate only the centroids it keeps in float64
 hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, const double* C64T,
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
                           double* stats, int n_cu, const int* gate, hipStream_t s, double* sse = nullptr,
                           const uint32_t* cand = nullptr, uint32_t cand_cap = 0, int delta = 0,
-                          const float* sse_c32 = nullptr, uint2* chg = nullptr, const uint32_t* chg_cnt = nullptr);
+                          const float* sse_c32 = nullptr, uint2* chg = nullptr, const uint32_t* chg_cnt = nullptr,
+                          const float* C32 = nullptr, const float* cmax = nullptr);
 // Fused assign + partial sums (kp*dp <= 16384 class): fp16 hi image in VGPRs,
 // lo image + float64 sum table in LDS; decided points summed here, queued
 // points (and their counts) by launch_resolve(stats).

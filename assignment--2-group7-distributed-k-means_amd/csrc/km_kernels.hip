@@ -3879,7 +3879,17 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
 // each of its G points in NumPy's order (np_norm), from the chunk (one
 // conflict-free double per lane) and the point's row staged in LDS
 // (broadcast reads).  Full-scan entries sit at the back of each segment.
-template <int G, bool WIDE>  // WIDE: d > 256, no LDS chunks (ch = 0)
+// PF (fp32 prefilter, d <= 256 with the fp32 images C32 [kp][dp] and their
+// largest norm *cmax): the scan runs in fp32 first -- D~ = sum (x - c')^2 from
+// fp32 chunks of the images in LDS (packed differences and fmas), its bounds
+// [L, U] on ||x - c|| as in k_s1's re-score (sum rounding (d/2 + 8) u,
+// sqrt 4 u, ||c - c'|| <= u cmax) -- and a point keeps, per chunk, the
+// centroids whose L is under the smallest U so far (the running minimum only
+// falls, so the true argmin is kept: its L is under every U).  Those (<= 64)
+// are then evaluated in float64 in NumPy's order, one per lane, and the
+// usual argmin decides.  A point with a non-finite row, non-finite
+// centroids or more than 64 kept centroids takes the float64 chunk pass.
+template <int G, bool WIDE, bool PF = false>  // WIDE: d > 256, no LDS chunks (ch = 0)
 __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, int dp, int d, int k,
                                                    const double* __restrict__ C64T, const QEntry* __restrict__ queue,
                                                    const uint32_t* __restrict__ qcount, QLayout ql,
@@ -3887,12 +3897,17 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
                                                    double* __restrict__ stats, int use_chain, int pair_chain,
                                                    double* __restrict__ sse, const int* __restrict__ gate, int delta,
                                                    const float* __restrict__ sse_c32, uint2* __restrict__ chg,
-                                                   const uint32_t* __restrict__ chg_cnt) {
+                                                   const uint32_t* __restrict__ chg_cnt,
+                                                   const float* __restrict__ C32, const float* __restrict__ cmax,
+                                                   const double* __restrict__ C64r) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sCT = reinterpret_cast<double*>(smem);                                    // [d][ch]
   float* xs_all = reinterpret_cast<float*>(smem + (size_t)d * ch * 8);              // [8][G][d]
   uint32_t* pre = reinterpret_cast<uint32_t*>(smem + (size_t)d * ch * 8 + (size_t)8 * G * d * 4);
+  // PF: the kept centroids [8][G][64] behind the prefix (16-B aligned)
+  uint32_t* kept_all = pre + ((ql.nwaves + 1u + 3u) & ~3u);
+  const float cmv = PF ? *cmax : 0.0f;
   block_prefix(qcount, 1, ql.nwaves, pre);
   const uint32_t total = pre[ql.nwaves];
   const int lane = threadIdx.x & 63;
@@ -4023,6 +4038,115 @@ __global__ __launch_bounds__(512) void k_fullscan(const float* __restrict__ X, i
       finish(g, bv, bi);
       have[g] = false;
     }
+    if constexpr (PF) {
+      // fp32 prefilter (see above): the wave's points with finite rows
+      bool ok[G];
+      bool any = false;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        bool fin = true;
+        for (int f = lane; f < d; f += 64) fin = fin && (fabsf(xs[g * d + f]) <= 3.0e38f);
+        ok[g] = have[g] && (cmv <= 3.0e38f) && __ballot(!fin) == 0ull;
+        any |= ok[g];
+      }
+      if (__syncthreads_or(any)) {
+        uint32_t* kept = kept_all + (size_t)wave * G * 64;
+        float ust[G];
+        uint32_t nk[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          ust[g] = FLT_MAX;
+          nk[g] = 0u;
+        }
+        const int cs2 = ch + 1;  // f32x2 row stride of the chunk (bank spread of the transposed writes)
+        const float e = ((float)(d / 2 + 8) * 0.5f + 8.0f) * U24 * 1.1f;
+        const float gam = U24 * cmv * 1.01f + 1e-37f;
+        typedef float f32x2_t __attribute__((ext_vector_type(2)));
+        f32x2_t* sC = reinterpret_cast<f32x2_t*>(sCT);  // [d/2][ch + 1] feature pairs
+        // chunk staging: float4 pieces of the images' rows (dp a power of
+        // two: Q pieces per row), the next chunk's loads in flight in
+        // registers while this one is scanned
+        const int Q = dp >> 2, lq = __builtin_ctz((unsigned)Q), nf4 = ch * Q;
+        const float4* C32v = reinterpret_cast<const float4*>(C32);
+        float4 nv[4];
+        auto fetch = [&](int c0) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int idx = threadIdx.x + t * (int)blockDim.x;
+            const int jj = idx >> lq, q4 = idx & (Q - 1);
+            nv[t] = (idx < nf4 && c0 + jj < k) ? C32v[(size_t)(c0 + jj) * Q + q4] : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        };
+        auto put = [&]() {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int idx = threadIdx.x + t * (int)blockDim.x;
+            const int jj = idx >> lq, q4 = idx & (Q - 1), p0 = 2 * q4;  // feature pairs p0, p0 + 1
+            if (idx < nf4 && 2 * p0 < d) sC[p0 * cs2 + jj] = f32x2_t{nv[t].x, nv[t].y};
+            if (idx < nf4 && 2 * p0 + 2 < d) sC[(p0 + 1) * cs2 + jj] = f32x2_t{nv[t].z, nv[t].w};
+          }
+        };
+        fetch(0);
+        for (int c0 = 0; c0 < k; c0 += ch) {
+          __syncthreads();  // the previous chunk is scanned
+          const int cw = min(ch, k - c0);
+          put();
+          if (c0 + ch < k) fetch(c0 + ch);
+          __syncthreads();
+          f32x2_t acc[G];
+#pragma unroll
+          for (int g = 0; g < G; ++g) acc[g] = f32x2_t{0.0f, 0.0f};
+#pragma unroll 4
+          for (int fp = 0; fp < (d >> 1); ++fp) {
+            const f32x2_t c2 = sC[fp * cs2 + lane];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+              const f32x2_t x2 = reinterpret_cast<const f32x2_t*>(xs + g * d)[fp];
+              const f32x2_t df = x2 - c2;
+              acc[g] = __builtin_elementwise_fma(df, df, acc[g]);
+            }
+          }
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            if (!ok[g]) continue;
+            const bool in = lane < cw;
+            const float Dt = acc[g].x + acc[g].y;
+            const bool tiny = !(Dt >= 0x1p-96f);
+            const float r = __builtin_amdgcn_sqrtf(tiny ? 0x1p-96f : Dt);
+            const float U = in ? fmaf(r, 1.0f + e, gam) * (1.0f + 4.0f * U24) : FLT_MAX;
+            const float L = in ? fmaf(tiny ? 0.0f : r, 1.0f - e, -gam) * (1.0f - 4.0f * U24) : FLT_MAX;
+            float um = U;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) um = fminf(um, __shfl_xor(um, o));
+            ust[g] = fminf(ust[g], um);
+            const bool keep = in && L <= ust[g] * (1.0f + 8.0f * U24);
+            const uint64_t m = __ballot(keep);
+            const uint32_t nm = (uint32_t)__popcll(m);
+            if (nk[g] + nm <= 64u && keep)
+              kept[g * 64 + nk[g] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)(c0 + lane);
+            nk[g] += nm;
+          }
+        }
+        __syncthreads();  // the kept lists are visible to every lane
+        // the kept centroids in float64, NumPy's order, one per lane
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          if (!ok[g] || nk[g] > 64u) continue;  // more kept: the float64 chunk pass below
+          const bool act = (uint32_t)lane < nk[g];
+          const int j = act ? (int)kept[g * 64 + lane] : 0;
+          const float* xg = xs + g * d;
+          double bv = 0.0;
+          int bi = -1;
+          if (act) {
+            const double* cj = C64r + (size_t)j * d;  // row-major: one contiguous row per lane
+            bv = np_norm_d<2>([&](int f) { return np_sq(cj[f], xg[f]); }, d);
+            bi = j;
+          }
+          finish(g, bv, bi);
+          have[g] = false;
+        }
+      }
+    }
     double best[G];
     int bj[G];
     bool any_full = false;
@@ -4117,7 +4241,7 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
                           const QEntry* queue, const uint32_t* qcount, const QLayout& ql, int32_t* labels,
                           double* stats, int n_cu, const int* gate, hipStream_t s, double* sse,
                           const uint32_t* cand, uint32_t cand_cap, int delta, const float* sse_c32, uint2* chg,
-                          const uint32_t* chg_cnt) {
+                          const uint32_t* chg_cnt, const float* C32, const float* cmax) {
   if (g.n == 0 || ql.nwaves == 0) return hipSuccess;
   if (delta && (!chg || !chg_cnt || g.k > 65535)) return hipErrorInvalidValue;
   if (delta) stats = nullptr;  // the moves go to the change list
@@ -4132,7 +4256,13 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   static const int fs_g = diag_env("KM_FS_G", 0);
   const int G = fs_g == 4 ? 4 : (fs_g == 2 ? 2 : (g.k > 256 ? 4 : 2));
   const int ch = g.d <= 128 ? 64 : (g.d <= 256 ? 32 : 0);  // chunk columns (<= 64 KiB of LDS); 0: direct
-  const size_t fs_lds = (size_t)g.d * ch * 8 + (size_t)8 * G * g.d * 4 + pre_bytes;
+  // fp32 prefilter of the full scans (KM_FS_PF, default on) where the images
+  // are given: + the kept lists [8][G][64] behind the 16-B aligned prefix
+  static const int fs_pf = diag_env("KM_FS_PF", 1);
+  const bool pf = fs_pf && ch > 0 && C32 != nullptr && cmax != nullptr && g.d % 2 == 0 &&
+                  (g.dp == 32 || g.dp == 64 || g.dp == 128 || g.dp == 256) && (size_t)ch * g.dp / 4 <= 4 * 512;
+  const size_t fs_lds = (size_t)g.d * ch * 8 + (size_t)8 * G * g.d * 4 +
+                        (pf ? (((size_t)ql.nwaves + 4) & ~(size_t)3) * 4 + (size_t)8 * G * 64 * 4 : pre_bytes);
   if (fs_lds > LDS_MAX) return hipErrorInvalidValue;
   static const int use_chain = diag_env("KM_CHAIN", 1);
   static const int pair_chain = diag_env("KM_PAIR_CHAIN", 1);
@@ -4140,15 +4270,23 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   if (ch == 0)
     hipLaunchKernelGGL((k_fullscan<2, true>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
                        queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, sse, gate, delta, sse_c32, chg,
-                       chg_cnt);
+                       chg_cnt, C32, cmax, C64);
+  else if (G == 4 && pf)
+    hipLaunchKernelGGL((k_fullscan<4, false, true>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k,
+                       C64T, queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, sse, gate, delta,
+                       sse_c32, chg, chg_cnt, C32, cmax, C64);
   else if (G == 4)
     hipLaunchKernelGGL((k_fullscan<4, false>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
                        queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, sse, gate, delta, sse_c32, chg,
-                       chg_cnt);
+                       chg_cnt, C32, cmax, C64);
+  else if (pf)
+    hipLaunchKernelGGL((k_fullscan<2, false, true>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k,
+                       C64T, queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, sse, gate, delta,
+                       sse_c32, chg, chg_cnt, C32, cmax, C64);
   else
     hipLaunchKernelGGL((k_fullscan<2, false>), dim3(n_cu * fs_wg), dim3(512), fs_lds, s, X, g.dp, g.d, g.k, C64T,
                        queue, qcount, ql, labels, ch, (double*)nullptr, use_chain, pair_chain, sse, gate, delta, sse_c32, chg,
-                       chg_cnt);
+                       chg_cnt, C32, cmax, C64);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t tab_bytes = (size_t)(g.d + 1) * g.kp * 8;

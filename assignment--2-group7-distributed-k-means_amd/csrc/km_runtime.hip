@@ -592,7 +592,7 @@ int run_assign(km_ctx* c, bool with_stats) {
       ProfScope ps(c, KM_K_RESOLVE);
       KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels, nullptr,
                                 c->n_cu, c->gate, c->stream, s1_sse, nullptr, 0, with_stats ? 1 : 0,
-                                s1_sse ? c->C32 : nullptr, c->chg, c->chg_cnt));
+                                s1_sse ? c->C32 : nullptr, c->chg, c->chg_cnt, c->C32, c->cmax));
     }
     if (with_stats) {
       // the rows k_s1 moved between clusters (its change list) into the deltas
@@ -625,7 +625,7 @@ int run_assign(km_ctx* c, bool with_stats) {
       ProfScope ps(c, KM_K_RESOLVE);
       KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels,
                                 with_stats ? c->stats : nullptr, c->n_cu, c->gate, c->stream,
-                                sse ? sse_slot : nullptr));
+                                sse ? sse_slot : nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr, c->C32, c->cmax));
     }
     return KM_OK;  // counts are part of the fused and resolver statistics
   }
@@ -641,7 +641,8 @@ int run_assign(km_ctx* c, bool with_stats) {
     {
       ProfScope ps(c, KM_K_RESOLVE);
       KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels, nullptr,
-                                c->n_cu, c->gate, c->stream));
+                                c->n_cu, c->gate, c->stream, nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr, c->C32,
+                                c->cmax));
     }
   } else {
   if (!c->cand && g.dp <= 256) {
@@ -676,7 +677,7 @@ int run_assign(km_ctx* c, bool with_stats) {
     ProfScope ps(c, KM_K_RESOLVE);
     KM_HIP(km::launch_resolve(c->X, g, c->C64_cur, c->C64T, c->queue, c->qcount, c->ql, c->labels, nullptr, c->n_cu,
                               c->gate, c->stream, nullptr, c->cand, c->cand_cap, mdelta ? 1 : 0, nullptr,
-                              mdelta ? c->chg_m : nullptr, mdelta ? c->chg_m_cnt : nullptr));
+                              mdelta ? c->chg_m : nullptr, mdelta ? c->chg_m_cnt : nullptr, c->C32, c->cmax));
   }
   if (mdelta) {
     ProfScope ps(c, KM_K_STATS);

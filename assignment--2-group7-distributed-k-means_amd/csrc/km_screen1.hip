@@ -1055,14 +1055,21 @@ __global__ __launch_bounds__(1024) void k_s1_delta(const float* __restrict__ X, 
   const uint32_t span = min((uint32_t)kr, (uint32_t)k - lo);
   for (int i = threadIdx.x; i < (int)span * d1; i += blockDim.x) tab[i] = 0.0;
   __syncthreads();
-  // entry e of the concatenation: segment w = the last with pre[w] <= e
-  auto at = [&](uint32_t e) {
-    int a = 0, h = nw - 1;
-    while (a < h) {
-      const int mid = (a + h + 1) >> 1;
-      if (pre[mid] <= e) a = mid; else h = mid - 1;
+  // entry e of the concatenation: segment w = the last with pre[w] <= e; a
+  // lane's entries only grow, so after one binary search its segment is
+  // found by walking forward (a step or two per window)
+  int sgl = 0;
+  {
+    const uint32_t e = min(e0 + (uint32_t)wave * 64u + (uint32_t)lane, nc - 1u);
+    int h = nw - 1;
+    while (sgl < h) {
+      const int mid = (sgl + h + 1) >> 1;
+      if (pre[mid] <= e) sgl = mid; else h = mid - 1;
     }
-    return chg[(size_t)a * seg + (e - pre[a])];
+  }
+  auto at = [&](uint32_t e) {
+    while (sgl + 1 < nw && pre[sgl + 1] <= e) ++sgl;
+    return chg[(size_t)sgl * seg + (e - pre[sgl])];
   };
   for (uint32_t base = e0 + (uint32_t)wave * 64u; base < e1; base += (uint32_t)nwv * 64u) {
     const uint32_t e = base + (uint32_t)lane;

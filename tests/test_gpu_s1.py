@@ -543,3 +543,31 @@ def test_one_mfma_unfused_poor_seeds_delta_statistics():
     ref = orc.lloyd_fit(X, k, 4, 1e-12, 0, False, 1, init_centroids=C0, empty_seed=lambda: SEED)
     assert ref["records"][0]["empty"]
     np.testing.assert_allclose(km.centroids, ref["centroids"], rtol=1e-9, atol=1e-9)
+
+
+# -- the full scans' fp32 prefilter (k_fullscan<..., PF>) ---------------------------------
+
+@pytest.mark.parametrize("d,k,group", [
+    (128, 4096, 20),   # c5 geometry: <= 64 kept, float64 on the kept ones
+    (128, 4096, 80),   # more than 64 kept: the float64 chunk pass
+    (64, 256, 24),     # c3 geometry (k_s1's full scans)
+    (32, 1024, 40),    # c4 geometry
+    (96, 640, 30),     # dp 96: the fp16x3 screen's full scans
+])
+def test_full_scan_prefilter_equidistant_groups(d, k, group):
+    # rows with a group of centroids at the same distance up to float64
+    # rounding: no screen separates them, the full scan's fp32 prefilter keeps
+    # the whole group (its bounds overlap), and the float64 NumPy-order norms
+    # pick the reference's argmin -- including the lowest-index tie-break
+    rng = np.random.default_rng(d + k + group)
+    nrow = 3000
+    X = rng.uniform(-5, 5, (nrow, d)).astype(np.float32).astype(np.float64)
+    C = rng.uniform(-5, 5, (k, d))
+    ng = min(64, k // group)
+    for i in range(ng):
+        u = rng.standard_normal((group, d))
+        u /= np.linalg.norm(u, axis=1, keepdims=True)
+        C[i * group:(i + 1) * group] = X[i] + 0.5 * u
+    C[ng * group] = C[0]  # an exact duplicate: the lower index wins
+    a, eng = _predict(X, C)
+    np.testing.assert_array_equal(a, orc.assign(X, C)[0])
