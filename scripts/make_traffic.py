@@ -44,5 +44,7 @@ db[cfg] = {
     "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, python3 bench.py --config {cfg} "
               "--steps 3 --warmup 1 --no-cpu-baseline (1 x MI355X)",
 }
+if os.environ.get("ROUND"):
+    db[cfg]["round"] = int(os.environ["ROUND"])
 json.dump(db, open(out, "w"), indent=1)
 print(json.dumps(db[cfg], indent=1))
