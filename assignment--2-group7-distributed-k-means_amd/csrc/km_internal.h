@@ -148,7 +148,6 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
 // points (and their counts) by launch_resolve(stats).
 bool fused_path_ok(const Geometry& g);
 #ifdef KM_DIAG
-void dump_fused_stamps();  // diagnostic build only (KM_ABLATE=7)
 #endif
 // Tuning / ablation knob `name`: read from the environment only in the
 // diagnostic build (make diag, -DKM_DIAG); the product library always uses

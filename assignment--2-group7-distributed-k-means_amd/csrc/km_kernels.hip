@@ -374,9 +374,6 @@ __device__ void update_one_body(double* __restrict__ stats, const double* __rest
 #ifndef KM_SMALL_NTL  // labels stored non-temporal: +1% (the 40 MB of labels leave the cache to X)
 #define KM_SMALL_NTL 1
 #endif
-#ifndef KM_SMALL_ABL  // timing ablations only (wrong sums): 1 no global flush, 2 no statistics at all
-#define KM_SMALL_ABL 0
-#endif
 template <int DP, bool SSE, int WPE = (DP <= 16 ? KM_SMALL_WPE : 1)>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const float* __restrict__ C32,
@@ -503,7 +500,7 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
         }
       sacc += r;
     }
-    if (fuse && KM_SMALL_ABL < 2) {
+    if (fuse) {
       double* t = tab + (size_t)lab * d1 * R + rep;
 #pragma unroll
       for (int f = 0; f < DP; ++f)
@@ -623,7 +620,7 @@ void k_assign_small(const float* __restrict__ X, int64_t n, int d, int k, const 
     for (int e = threadIdx.x; e < k * d1; e += blockDim.x) {
       double s = 0.0;
       for (int r = 0; r < R; ++r) s += tab[(size_t)e * R + r];
-      if (s != 0.0 && KM_SMALL_ABL == 0) atomicAdd(stats + e, s);
+      if (s != 0.0) atomicAdd(stats + e, s);
     }
   }
   // ---- the last workgroup: queued rows, then (fold) the update ----
@@ -863,12 +860,10 @@ struct MfmaArgs {
 // A fragment is one contiguous 1 KiB piece, lane l at byte 16*l (rows
 // 32b + (l&31), features 16t + 8(l>>5) .. +8): lane-linear, bank-conflict
 // free, and every read of a block is base + immediate offset.
-// ABL (diagnostic builds only, never selected by default): 1 = no key
-// updates, 2 = no MFMAs (labels are then wrong; timing only).
 // T2: chains keep their best two keys (3 VALU per score instead of 4; for
 // small d, where the key updates, not the MFMAs, bound the loop); a point
 // whose best two share a chain then has no re-rank certificate (full scan).
-template <int NS, int WAVES, int ABL = 0, bool T2 = false>
+template <int NS, int WAVES, bool T2 = false>
 __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_assign_mfma(MfmaArgs A) {
   if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   constexpr int DP = 16 * NS;
@@ -1014,37 +1009,10 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
       const size_t off = (size_t)blk * BLKB + (size_t)t * 1024;
       Frag f;
       f.hi = *reinterpret_cast<const f16x8*>(laneHi + off);
-      if constexpr (ABL == 3)
-        f.lo = f.hi;  // diagnostic: half the LDS fragment reads
-      else
-        f.lo = *reinterpret_cast<const f16x8*>(laneLo + off);
+      f.lo = *reinterpret_cast<const f16x8*>(laneLo + off);
       return f;
     };
     auto mfma3 = [&](f32x16 acc, const Frag& f, int t) {
-      if constexpr (ABL == 2) {
-        acc[t] += (float)f.hi[0] + (float)f.lo[1] + (float)bl[t][2] + (float)bh[t][3];
-        return acc;
-      }
-      if constexpr (ABL == 4) {
-        // diagnostic (results wrong): the same MACs on v_mfma_f32_16x16x32_f16
-        // (two per 32x32x16, the same operand registers, four 4-register
-        // accumulators in the 16 of acc) -- the shape's clock lever in this
-        // kernel, with no key updates (compare ABL = 1)
-        f32x4 q[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) q[i] = f32x4{acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]};
-        q[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.hi, bl[t], q[0], 0, 0, 0);
-        q[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.hi, bl[t], q[1], 0, 0, 0);
-        q[2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.lo, bh[t], q[2], 0, 0, 0);
-        q[3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.lo, bh[t], q[3], 0, 0, 0);
-        q[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.hi, bh[t], q[0], 0, 0, 0);
-        q[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.hi, bh[t], q[1], 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int e2 = 0; e2 < 4; ++e2) acc[4 * i + e2] = q[i][e2];
-        return acc;
-      }
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.hi, bl[t], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.lo, bh[t], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.hi, bh[t], acc, 0, 0, 0);
@@ -1061,11 +1029,6 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
       }
     };
     auto key_update = [&](const f32x16& acc, int reg) {
-      if constexpr (ABL == 1 || ABL == 4) {
-        if (reg == 0) a1[0] = fminf(a1[0], acc[0] + acc[15]);
-        asm volatile("" ::"v"(acc[reg]));
-        return;
-      }
       const float key = __uint_as_float((__float_as_uint(acc[reg]) & ~maskq) | jg[reg >> 2]);
       if constexpr (T2) {
         const int c = reg & 3;
@@ -1097,7 +1060,7 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
       for (int t = 0; t < NS; ++t) {
         const Frag nx = (t + 1 < NS) ? load_frag(blk, t + 1) : load_frag(blk + 1 < nblk ? blk + 1 : blk, 0);
         cur = mfma3(cur, fr, t);
-        if constexpr (T2 && ABL != 1) {
+        if constexpr (T2) {
 #pragma unroll
           for (int pp = 0; pp < 8; ++pp)
             if (pp * NS / 8 == t) key_pair(prev, pp);
@@ -1145,7 +1108,7 @@ __global__ __launch_bounds__(WAVES * 64, (mfma_min_waves<NS, WAVES>())) void k_a
       set_jg(jq0 + 8u * (uint32_t)(blk - 1));
       overlapped(accB, blk, nb, accA);
       set_jg(jq0 + 8u * (uint32_t)blk);
-      if constexpr (T2 && ABL != 1) {
+      if constexpr (T2) {
 #pragma unroll
         for (int pp = 0; pp < 8; ++pp) key_pair(accB, pp);
       } else {
@@ -2174,33 +2137,16 @@ static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, con
   if constexpr (NS <= 4) {
     if (mfma_top2(NS)) {
       if (waves == 4)
-        hipLaunchKernelGGL((k_assign_mfma<NS, 4, 0, true>), dim3(blocks), dim3(256), lds, s, a);
+        hipLaunchKernelGGL((k_assign_mfma<NS, 4, true>), dim3(blocks), dim3(256), lds, s, a);
       else if (waves == 16)
-        hipLaunchKernelGGL((k_assign_mfma<NS, 16, 0, true>), dim3(blocks), dim3(1024), lds, s, a);
+        hipLaunchKernelGGL((k_assign_mfma<NS, 16, true>), dim3(blocks), dim3(1024), lds, s, a);
       else if (waves == 12)
-        hipLaunchKernelGGL((k_assign_mfma<NS, 12, 0, true>), dim3(blocks), dim3(768), lds, s, a);
+        hipLaunchKernelGGL((k_assign_mfma<NS, 12, true>), dim3(blocks), dim3(768), lds, s, a);
       else
-        hipLaunchKernelGGL((k_assign_mfma<NS, 8, 0, true>), dim3(blocks), dim3(512), lds, s, a);
+        hipLaunchKernelGGL((k_assign_mfma<NS, 8, true>), dim3(blocks), dim3(512), lds, s, a);
       return;
     }
   }
-#ifdef KM_DIAG
-  if constexpr (NS == 8) {  // KM_ABLATE=11 (no key updates) | 12 (MFMA -> adds) | 13 (no lo reads)
-                            // | 15 (no key updates, 16x16x32 MFMAs), c5 shape
-    static const int e = diag_env("KM_ABLATE", 0);
-    if (waves == 12 && e >= 11 && e <= 15 && e != 14) {  // instead of the product kernel
-      if (e == 15)
-        hipLaunchKernelGGL((k_assign_mfma<NS, 12, 4>), dim3(blocks), dim3(768), lds, s, a);
-      else if (e == 11)
-        hipLaunchKernelGGL((k_assign_mfma<NS, 12, 1>), dim3(blocks), dim3(768), lds, s, a);
-      else if (e == 12)
-        hipLaunchKernelGGL((k_assign_mfma<NS, 12, 2>), dim3(blocks), dim3(768), lds, s, a);
-      else
-        hipLaunchKernelGGL((k_assign_mfma<NS, 12, 3>), dim3(blocks), dim3(768), lds, s, a);
-      return;
-    }
-  }
-#endif
   if constexpr (NS >= 12) {
     hipLaunchKernelGGL((k_assign_mfma<NS, 4>), dim3(blocks), dim3(256), lds, s, a);
   } else {
@@ -2215,15 +2161,6 @@ static void launch_mfma_ns(int waves, int blocks, size_t lds, hipStream_t s, con
       hipLaunchKernelGGL((k_assign_mfma<NS, 12>), dim3(blocks), dim3(768), lds, s, a);
     else
       hipLaunchKernelGGL((k_assign_mfma<NS, 8>), dim3(blocks), dim3(512), lds, s, a);
-#ifdef KM_DIAG
-    if constexpr (NS == 4) {  // diagnostic ablations (KM_ABLATE=1|2), c3 shape only
-      static const int e = diag_env("KM_ABLATE", 0);
-      if (e == 1)
-        hipLaunchKernelGGL((k_assign_mfma<NS, 12, 1>), dim3(blocks), dim3(768), lds, s, a);
-      else if (e == 2)
-        hipLaunchKernelGGL((k_assign_mfma<NS, 12, 2>), dim3(blocks), dim3(768), lds, s, a);
-    }
-#endif
   }
 }
 
@@ -2351,9 +2288,6 @@ __device__ __forceinline__ void merge3(float& K1, float& K2, float& K3, uint32_t
   K3 = n3;
 }
 
-// diagnostic stamp accumulators (ABL == 7 builds only): per-phase cycles
-__device__ unsigned long long g_stamp[8];
-
 struct FusedArgs {
   const float* X;
   const float* xnorm;  // per-row upper bound of ||x|| (unscaled)
@@ -2379,14 +2313,10 @@ struct FusedArgs {
 constexpr int ceil_log2_c(int v) { return v <= 1 ? 0 : 1 + ceil_log2_c((v + 1) / 2); }
 
 
-// ABL (diagnostic builds, KM_ABLATE=1..4, c3 shape only; results wrong):
-// 1 = no key updates, 2 = no MFMAs, 3 = no LDS sums, 4 = no merge / queue,
-// 5 = MFMAs + conversion + loads only, 6 = as 5 with L2-resident rows,
-// 7 = full kernel with s_memtime phase stamps, 8 = full kernel, compiler schedule
 // SSE (compute_sse, kmeans_spark.py:224-237): every decided row's float64
 // residual to its pre-update centroid (C64P, gathered from L2 by label) is
 // summed in the same pass; queued rows get theirs from the resolvers
-template <int NS, int NB, bool STATS, int ABL = 0, bool REF = true, bool SSE = false>
+template <int NS, int NB, bool STATS, bool REF = true, bool SSE = false>
 __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   constexpr int DP = 16 * NS;
@@ -2438,7 +2368,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   const float4* cnl = reinterpret_cast<const float4*>(sCn + 4 * h);  // + 8 blk + 2 g4
 
   auto load_tile = [&](int64_t tile, float4 (&xq)[NS][2], float& xnq) {
-    const int64_t row = (ABL == 6 ? (tile & 7) : tile) * 32 + r;
+    const int64_t row = tile * 32 + r;
     const int64_t rr = row < n ? row : (n - 1);
     const float* xr = A.X + rr * DP + 8 * h;
 #pragma unroll
@@ -2449,9 +2379,6 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
     xnq = A.xnorm[rr];
   };
 
-  unsigned long long st_acc[5] = {0, 0, 0, 0, 0};
-  unsigned long long st_last = 0;
-  if constexpr (ABL == 7) st_last = __builtin_amdgcn_s_memtime();
   double ss_acc = 0.0;  // SSE variant: this lane's residual sum
   auto process_tile = [&](int64_t tile, const float4 (&xc)[NS][2], float xn) {
     const int64_t row = tile * 32 + r;
@@ -2478,13 +2405,6 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
         bl[t][e + 1] = lo[1];
       }
     }
-    if constexpr (ABL == 7) {
-      __builtin_amdgcn_sched_barrier(0);
-      const unsigned long long tnow = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_sched_barrier(0);
-      st_acc[0] += tnow - st_last;
-      st_last = tnow;
-    }
     float a1[4], a2[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) a1[c] = a2[c] = FLT_MAX;
@@ -2507,11 +2427,6 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       return acc;
     };
     auto mfma_block = [&](f32x16 acc, int blk) {
-      if constexpr (ABL == 2) {
-#pragma unroll
-        for (int t = 0; t < NS; ++t) acc[t] += (float)Ahi[blk][t][0] + (float)Alo[blk][t][1] + (float)bl[t][2] + (float)bh[t][3];
-        return acc;
-      }
 #pragma unroll
       for (int t = 0; t < NS; ++t) {
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ahi[blk][t], bl[t], acc, 0, 0, 0);
@@ -2524,11 +2439,6 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
     // chain reg & 3 keeps the top two keys (score | j >> 2); registers reg and
     // reg + 4 (same chain) are folded in together
     auto keys_block = [&](const f32x16& acc, int blk) {
-      if constexpr (ABL == 1 || ABL == 5 || ABL == 6) {
-        a1[blk & 3] = fminf(a1[blk & 3], acc[0] + acc[15]);
-        asm volatile("" ::"v"(acc));
-        return;
-      }
       const uint32_t jq = (uint32_t)(8 * blk + h);
       // two keys of one chain per step: new best = min3(best, ka, kb), new
       // second = min(second, med3(best, ka, kb)) -- the same top two as one
@@ -2558,7 +2468,6 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       accs[blk & 1] = mfma_block(cin, blk);
       keys_block(accs[(blk - 1) & 1], blk - 1);
       // MFMA, next block's init reads, MFMA, then (VALU x m, MFMA) pairs
-      if constexpr (ABL == 8) continue;  // diagnostic: compiler's own schedule
       __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
       __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
@@ -2570,34 +2479,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       __builtin_amdgcn_sched_barrier(0);
     }
     keys_block(accs[(NB - 1) & 1], NB - 1);
-    if constexpr (ABL == 7) {
-      __builtin_amdgcn_sched_barrier(0);
-      const unsigned long long tnow = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_sched_barrier(0);
-      st_acc[1] += tnow - st_last;
-      st_last = tnow;
-    }
 
-    if constexpr (ABL == 5 || ABL == 6) {
-      const int lab = (int)(__float_as_uint(a1[0] + a1[1] + a1[2] + a1[3] + xn) & 255u) % A.k;
-      if (h == 0 && valid) A.labels[row] = lab;
-      return;
-    }
-    if constexpr (ABL == 4) {
-      const int lab = (int)(__float_as_uint(a1[0] + a1[1] + a1[2] + a1[3] + a2[0] + a2[1] + a2[2] + a2[3] + xn) & 255u) % A.k;
-      if (h == 0 && valid) A.labels[row] = lab;
-      if constexpr (STATS) {
-        double* tp = tab + (size_t)(8 * h) * TS + lab;
-#pragma unroll
-        for (int t = 0; t < NS; ++t) {
-          const float4 v0 = xc[t][0], v1 = xc[t][1];
-          const float xe[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-          for (int e = 0; e < 8; ++e) atomicAdd(tp + (size_t)(16 * t + e) * TS, (double)xe[e]);
-        }
-      }
-      return;
-    }
     // top-3 values and best two full indices: chains merged pairwise, then
     // the two lane halves.  A chain keeps its best two; keys it dropped are
     // only known to be >= its second, which therefore stands in for its
@@ -2667,13 +2549,6 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       const float thr3x = 2.0f * B0 + rho * (fabsf(k1) + fabsf(o));
       if (kind == 2u && same_chain && (o - k1 > thr3x || (REF && kb.lower(o) > u1))) kind = 3u;
     }
-    if constexpr (ABL == 7) {
-      __builtin_amdgcn_sched_barrier(0);
-      const unsigned long long tnow = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_sched_barrier(0);
-      st_acc[2] += tnow - st_last;
-      st_last = tnow;
-    }
     const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
     if (h == 0 && valid) A.labels[row] = lab;
     const bool enq = (h == 0) && valid && (kind != 0);
@@ -2696,14 +2571,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
       qn += (uint32_t)__popcll(m1);
       qf += (uint32_t)__popcll(m2);
     }
-    if constexpr (ABL == 7) {
-      __builtin_amdgcn_sched_barrier(0);
-      const unsigned long long tnow = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_sched_barrier(0);
-      st_acc[3] += tnow - st_last;
-      st_last = tnow;
-    }
-    if constexpr (STATS && ABL != 3) {
+    if constexpr (STATS) {
       if (valid && kind == 0) {
         double* tp = tab + (size_t)(8 * h) * TS + lab;
 #pragma unroll
@@ -2739,13 +2607,6 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
         }
       }
     }
-    if constexpr (ABL == 7) {
-      __builtin_amdgcn_sched_barrier(0);
-      const unsigned long long tnow = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_sched_barrier(0);
-      st_acc[4] += tnow - st_last;
-      st_last = tnow;
-    }
   };
 
   // tiles of this wave, two register buffers: the next tile's rows are in
@@ -2771,10 +2632,6 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
   if constexpr (SSE) {
     ss_acc = wave_sum(ss_acc);
     if (lane == 0 && ss_acc != 0.0) atomicAdd(A.sse, ss_acc);
-  }
-  if constexpr (ABL == 7) {
-    if (lane == 0)
-      for (int i = 0; i < 5; ++i) atomicAdd(&g_stamp[i], st_acc[i]);
   }
   if constexpr (STATS) {
     __syncthreads();
@@ -3238,9 +3095,9 @@ __global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
   }
 }
 
-// The diagnostic build's experimental kernels -- k_fusedp (software-pipelined
-// fused kernel) and the fast screen k_fused1 / k_prep_bal -- live in
-// km_diag.inc, compiled only by `make diag`.
+// The diagnostic build's experimental kernels -- the fast screen k_fused1 /
+// k_prep_bal -- live in km_diag.inc, compiled only by `make diag` (DESIGN.md
+// section 4).
 #ifdef KM_DIAG
 #include "km_diag.inc"
 #endif
@@ -3383,32 +3240,6 @@ __global__ __launch_bounds__(256) void k_row_norm_any(const float* __restrict__ 
   }
 }
 
-#ifdef KM_DIAG
-// diagnostic: print and clear the ABL=7 phase stamps (cycles summed over waves)
-void dump_fused_stamps() {
-  unsigned long long v[8];
-  const hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_stamp), sizeof(v));
-  if (e != hipSuccess) {
-    fprintf(stderr, "[km stamps] read failed: %s\n", hipGetErrorString(e));
-    return;
-  }
-  unsigned long long tot = 0;
-  for (int i = 0; i < 5; ++i) tot += v[i];
-  fprintf(stderr, "[km stamps] raw %llu %llu %llu %llu %llu %llu\n", v[0], v[1], v[2], v[3], v[4], v[5]);
-  if (tot == 0) return;
-  if (v[5]) {  // KM_ABLATE=9 (k_fusedp): head / region / tail per wave, kernel cycles, realtime ticks, waves
-    fprintf(stderr, "[km stamps] k_fusedp per wave: head %.0f region %.0f tail %.0f kernel %.0f cycles; "
-                    "clock %.3f GHz\n", (double)v[0] / v[5], (double)v[1] / v[5], (double)v[2] / v[5],
-            (double)v[3] / v[5], v[4] ? (double)v[3] / (double)v[4] * 0.1 : 0.0);
-  } else {
-    fprintf(stderr, "[km stamps] split %.3f blocks %.3f merge %.3f queue %.3f sums %.3f (fractions)\n",
-            (double)v[0] / tot, (double)v[1] / tot, (double)v[2] / tot, (double)v[3] / tot, (double)v[4] / tot);
-  }
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z));
-}
-#endif
-
 bool fused_path_ok(const Geometry& g) {
   const int ns = g.dp / 16, nb = g.kp / 32;
   if (g.dp % 16 || g.kp % 64) return false;
@@ -3511,40 +3342,17 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
                 C64P, sse, pairs};
   const size_t lds = (size_t)g.kp * 4 + (with_stats ? (size_t)(g.dp + 1) * g.kp * 8 : 0);
   [[maybe_unused]] const size_t lds_pair = (size_t)g.kp * (KM_PAIR_M + 1) * 4;
-#ifdef KM_DIAG
-  const size_t lds_p = (size_t)g.kp * 4 + (size_t)(g.dp + 1) * (g.kp + 1) * 8;  // k_fusedp: discard column
-#endif
 #define KM_FUSED_CASE(NS_, NB_)                                                                        \
   case NS_ * 100 + NB_:                                                                                \
     if (with_stats && sse)                                                                             \
-      KM_TIMED_LAUNCH((k_fused<NS_, NB_, true, 0, true, true>), dim3(nbk), dim3(256), lds, s, a);   \
+      KM_TIMED_LAUNCH((k_fused<NS_, NB_, true, true, true>), dim3(nbk), dim3(256), lds, s, a);   \
     else if (with_stats && !refine)                                                                    \
-      KM_TIMED_LAUNCH((k_fused<NS_, NB_, true, 0, false>), dim3(nbk), dim3(256), lds, s, a);        \
+      KM_TIMED_LAUNCH((k_fused<NS_, NB_, true, false>), dim3(nbk), dim3(256), lds, s, a);        \
     else if (with_stats)                                                                               \
       KM_TIMED_LAUNCH((k_fused<NS_, NB_, true>), dim3(nbk), dim3(256), lds, s, a);                  \
     else                                                                                               \
       KM_TIMED_LAUNCH((k_fused<NS_, NB_, false>), dim3(nbk), dim3(256), lds, s, a);                 \
     break;
-#ifdef KM_DIAG
-  {
-    static const int abl = diag_env("KM_ABLATE", 0);
-    if (abl >= 1 && abl <= 10 && ns == 4 && nb == 8 && with_stats && !sse) {
-      switch (abl) {
-        case 1: KM_TIMED_LAUNCH((k_fused<4, 8, true, 1>), dim3(nbk), dim3(256), lds, s, a); break;
-        case 2: KM_TIMED_LAUNCH((k_fused<4, 8, true, 2>), dim3(nbk), dim3(256), lds, s, a); break;
-        case 3: KM_TIMED_LAUNCH((k_fused<4, 8, true, 3>), dim3(nbk), dim3(256), lds, s, a); break;
-        case 5: KM_TIMED_LAUNCH((k_fused<4, 8, true, 5>), dim3(nbk), dim3(256), lds, s, a); break;
-        case 7: KM_TIMED_LAUNCH((k_fused<4, 8, true, 7>), dim3(nbk), dim3(256), lds, s, a); break;
-        case 8: KM_TIMED_LAUNCH((k_fused<4, 8, true, 8>), dim3(nbk), dim3(256), lds, s, a); break;
-        case 6: KM_TIMED_LAUNCH((k_fused<4, 8, true, 6>), dim3(nbk), dim3(256), lds, s, a); break;
-        case 9: KM_TIMED_LAUNCH((k_fusedp<4, 8, false, true>), dim3(nbk), dim3(256), lds_p, s, a); break;
-        case 10: KM_TIMED_LAUNCH((k_fusedp<4, 8, false>), dim3(nbk), dim3(256), lds_p, s, a); break;
-        default: KM_TIMED_LAUNCH((k_fused<4, 8, true, 4>), dim3(nbk), dim3(256), lds, s, a); break;
-      }
-      return hipGetLastError();
-    }
-  }
-#endif
 #define KM_FUSED16_CASE(NS2_, NB_)                                                                      \
   case NS2_ * 100 + NB_:                                                                                \
     KM_PAIR_BRANCH(NS2_, NB_)                                                                           \
@@ -4323,9 +4131,7 @@ static constexpr int STATS_LDS = 156 * 1024;
 // The workgroup also owns a feature range [f0, f0 + fr) (blockIdx.z):
 // splitting the features instead of the clusters keeps X read once when
 // k (d+1) doubles exceed LDS but k (fr+1) fit (c4: 1024 clusters x 16 features).
-// PLAIN (diagnostic build, KM_ABLATE=14): LDS read-add-write instead of the
-// float64 LDS atomics (races: results wrong by design), to price the atomics
-template <bool PLAIN = false, bool SSE = false>
+template <bool SSE = false>
 __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int64_t n, int d, int dp, int k,
                                                 const int32_t* __restrict__ labels, double* __restrict__ stats,
                                                 int kr, int fr, int64_t rows_per_block, const double* __restrict__ C64P,
@@ -4404,17 +4210,10 @@ __global__ __launch_bounds__(1024) void k_stats(const float* __restrict__ X, int
         const int lab = labs[u];
         if (act && rr < nrow && lab >= c0 && lab < c1) {
           double* t = tab + (lab - c0) * RS + mm;
-          if constexpr (PLAIN) {
-            t[0] += (double)v[u].x;
-            t[L] += (double)v[u].y;
-            t[2 * L] += (double)v[u].z;
-            t[3 * L] += (double)v[u].w;
-          } else {
-            atomicAdd(t, (double)v[u].x);
-            atomicAdd(t + L, (double)v[u].y);
-            atomicAdd(t + 2 * L, (double)v[u].z);
-            atomicAdd(t + 3 * L, (double)v[u].w);
-          }
+          atomicAdd(t, (double)v[u].x);
+          atomicAdd(t + L, (double)v[u].y);
+          atomicAdd(t + 2 * L, (double)v[u].z);
+          atomicAdd(t + 3 * L, (double)v[u].w);
           if (sse) {  // padded features are 0 - 0
             const float4 c = cg[u];
             const double t0 = (double)v[u].x - (double)c.x, t1 = (double)v[u].y - (double)c.y;
@@ -4517,21 +4316,12 @@ hipError_t launch_stats(const float* X, const Geometry& g, const int32_t* labels
   if (bx > (g.n + min_rows - 1) / min_rows) bx = (g.n + min_rows - 1) / min_rows;
   int64_t rpb = (g.n + bx - 1) / bx;
   rpb = (rpb + 63) / 64 * 64;
-#ifdef KM_DIAG
-  static const int abl = diag_env("KM_ABLATE", 0);
-  if (abl == 14) {
-    hipLaunchKernelGGL((k_stats<true, false>), dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024), lds, s, X,
-                       g.n, g.d, g.dp, g.k, labels, stats, kr, fr, rpb, C64P, C32,
-                       C64P ? stats + (size_t)g.k * (g.d + 1) : (double*)nullptr, gate);
-    return hipGetLastError();
-  }
-#endif
   if (C64P)
-    hipLaunchKernelGGL((k_stats<false, true>), dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024), lds,
+    hipLaunchKernelGGL((k_stats<true>), dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024), lds,
                        s, X, g.n, g.d, g.dp, g.k, labels, stats, kr, fr, rpb, C64P, C32,
                        stats + (size_t)g.k * (g.d + 1), gate);
   else
-    hipLaunchKernelGGL((k_stats<false, false>), dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024),
+    hipLaunchKernelGGL((k_stats<false>), dim3((unsigned)bx, (unsigned)ranges, (unsigned)franges), dim3(1024),
                        lds, s, X, g.n, g.d, g.dp, g.k, labels, stats, kr, fr, rpb, C64P, C32, (double*)nullptr, gate);
   return hipGetLastError();
 }

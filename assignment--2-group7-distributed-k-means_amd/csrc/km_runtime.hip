@@ -802,9 +802,6 @@ int km_sync(km_ctx* c) {
     if (rcf != KM_OK) return rcf;
   }
   KM_HIP(hipStreamSynchronize(c->stream));
-#ifdef KM_DIAG
-  if (km::diag_env("KM_ABLATE", 0) == 7 || km::diag_env("KM_ABLATE", 0) == 9) km::dump_fused_stamps();
-#endif
   return KM_OK;
 }
 
