@@ -171,11 +171,7 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
                         const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,
                         double* stats, int with_stats, int mode, int n_cu, QLayout* ql, const int* gate,
                         hipStream_t s, const float* C32, const float* cmax, float* bal, const double* C64P,
-                        double* sse, uint32_t* pairs);
-// pair screen of k_fused16 (two MFMAs per product, DESIGN.md "Pair screen"):
-// on for this geometry, and the words of its neighbour table (0 if off)
-bool pair_ok(const Geometry& g);
-size_t pair_words(const Geometry& g);
+                        double* sse);
 // bound constants of the fused screen (the MFMA shape it runs on: fused16_ok)
 hipError_t launch_bound_consts(const float* cmax, const float* xabs, const float* cabs, const Geometry& g, float* bnd,
                                const int* gate, hipStream_t s);

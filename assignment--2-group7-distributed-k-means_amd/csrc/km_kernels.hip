@@ -24,16 +24,9 @@
 #ifndef KM_WIDE_WAVES
 #define KM_WIDE_WAVES 12
 #endif
-// pair screen (k_fused16): neighbour-list length per centroid, and the switch
-#ifndef KM_PAIR_M
-#define KM_PAIR_M 16
-#endif
 // k_rerank2 runs on KM_RERANK_PCT percent of n_cu workgroups
 #ifndef KM_RERANK_PCT
 #define KM_RERANK_PCT 100
-#endif
-#ifndef KM_PAIR
-#define KM_PAIR 0
 #endif
 
 namespace km {
@@ -2307,7 +2300,6 @@ struct FusedArgs {
   const int* gate;     // nonzero: a stopped batch, the launch is a no-op
   const double* C64P;  // SSE variant: float64 centroids padded [kp][dp] (L2-resident)
   double* sse;         // SSE variant: the SSE slot stats[k (d+1)]
-  const uint32_t* pairs = nullptr;  // pair screen: [kp][KM_PAIR_M] neighbour table, then rmax [kp] (k_pair_table)
 };
 
 constexpr int ceil_log2_c(int v) { return v <= 1 ? 0 : 1 + ceil_log2_c((v + 1) / 2); }
@@ -2664,7 +2656,7 @@ __global__ __launch_bounds__(256, 1) void k_fused(FusedArgs A) {
 // lanes l and l ^ 16 hold the top-3 and best two of row (l & 15) + 16 (l >> 5).
 // The bound is screen_b0's with the 16x16x32 accumulation model (chain_err).
 // ---------------------------------------------------------------------------
-template <int NS2, int NB, bool STATS, bool REF = true, bool SSE = false, bool PAIR = false>
+template <int NS2, int NB, bool STATS, bool REF = true, bool SSE = false>
 __global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
   if (*A.gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   constexpr int DP = 32 * NS2;
@@ -2675,14 +2667,10 @@ __global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
   static_assert(NB >= 2, "pipelined blocks");
   constexpr uint32_t maskq = (1u << (B - 2)) - 1u;
   constexpr int TS = KP;
-  constexpr int NMF = (PAIR ? 8 : 12) * NS2;  // MFMAs per block
-  static_assert(!PAIR || KP <= 256, "pair screen: 8 index bits");
+  constexpr int NMF = 12 * NS2;  // MFMAs per block
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* sCn = reinterpret_cast<float*>(smem);            // ||c||^2 s^2 [KP]
   double* tab = reinterpret_cast<double*>(smem + KP * 4);  // [DP + 1][TS]
-  // pair screen: neighbour lists [KP][KM_PAIR_M] and radii [KP] (k_pair_table)
-  uint32_t* sPair = reinterpret_cast<uint32_t*>(smem + KP * 4 + (STATS ? (DP + 1) * TS * 8 : 0));
-  const float* sRmax = reinterpret_cast<const float*>(sPair + KP * KM_PAIR_M);
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -2692,8 +2680,6 @@ __global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
   for (int i = threadIdx.x; i < KP; i += WAVES * 64) sCn[i] = A.cn2s[i];
   if constexpr (STATS)
     for (int i = threadIdx.x; i < (DP + 1) * TS; i += WAVES * 64) tab[i] = 0.0;
-  if constexpr (PAIR)
-    for (int i = threadIdx.x; i < KP * (KM_PAIR_M + 1); i += WAVES * 64) sPair[i] = A.pairs[i];
   f16x8 Ahi[NB][2][NS2], Alo[NB][2][NS2];
 #pragma unroll
   for (int b = 0; b < NB; ++b)
@@ -2744,10 +2730,8 @@ __global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
   auto process_tile = [&](int64_t tile, const float4 (&xc)[2][NS2][2], float xn) {
     const int64_t row = tile * 32 + prow;
     const bool valid = row < n;
-    // B operands: xs = hi + lo (fp16, RN), as in k_fused.  Pair screen: hi
-    // only, and ||xs - hi||^2 (fp32, each difference exact) per row group
+    // B operands: xs = hi + lo (fp16, RN), as in k_fused
     f16x8 bh[2][NS2], bl[2][NS2];
-    float er[2] = {0.0f, 0.0f};
 #pragma unroll
     for (int pg = 0; pg < 2; ++pg)
 #pragma unroll
@@ -2760,15 +2744,9 @@ __global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
           const f16x2 hp = {(_Float16)xs0, (_Float16)xs1};
           bh[pg][t][e] = hp[0];
           bh[pg][t][e + 1] = hp[1];
-          if constexpr (PAIR) {
-            const float r0 = xs0 - (float)hp[0], r1 = xs1 - (float)hp[1];
-            er[pg] = fmaf(r0, r0, er[pg]);
-            er[pg] = fmaf(r1, r1, er[pg]);
-          } else {
-            const f16x2 lo = split_lo(hp, xs0, xs1);
-            bl[pg][t][e] = lo[0];
-            bl[pg][t][e + 1] = lo[1];
-          }
+          const f16x2 lo = split_lo(hp, xs0, xs1);
+          bl[pg][t][e] = lo[0];
+          bl[pg][t][e + 1] = lo[1];
         }
       }
     float a1[2][4], a2[2][4];
@@ -2798,13 +2776,11 @@ __global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
         for (int pg = 0; pg < 2; ++pg) a.v[cb][pg] = ini[cb];
 #pragma unroll
       for (int t = 0; t < NS2; ++t) {
-        if constexpr (!PAIR) {
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb)
+        for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-            for (int pg = 0; pg < 2; ++pg)
-              a.v[cb][pg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ahi[blk][cb][t], bl[pg][t], a.v[cb][pg], 0, 0, 0);
-        }
+          for (int pg = 0; pg < 2; ++pg)
+            a.v[cb][pg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ahi[blk][cb][t], bl[pg][t], a.v[cb][pg], 0, 0, 0);
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
@@ -2919,31 +2895,8 @@ __global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
     // p1, p2 in one chain (j & 15): no re-rank certificate (see k_fused)
     const bool same_chain = ((p1 ^ p2) & 15u) == 0u;
     const float B0 = fmaf(alpha, xn, beta);
-    // pair screen: the row's fp16 rounding e = hi - xs enters key j as
-    // -2 s c'_j . e, so keys i, j move apart by at most 2 ||e|| s ||c'_i - c'_j||
-    // (DESIGN.md "Pair screen"): wE = 2 ||e|| (the row group's residuals
-    // summed over the four quarter lanes, identical in all four), times Dm =
-    // the largest distance from c'_p1 to any centroid, or the exact pair
-    // distance from p1's neighbour list
-    float wE = 0.0f, Dm = 0.0f;
-    if constexpr (PAIR) {
-      uint32_t lo, hi;
-      swap_halves(__float_as_uint(er[0]), __float_as_uint(er[1]), lo, hi);
-      const float eh = __uint_as_float(lo) + __uint_as_float(hi);
-      perm_quarters(__float_as_uint(eh), lo, hi);
-      wE = 2.0f * sqrtf((__uint_as_float(lo) + __uint_as_float(hi)) * 1.0001f) * 1.0001f;
-      // a centroid j that beats p1 is no farther from x than c'_p1 (up to the
-      // bound), so ||c'_j - c'_p1|| <= 2 d1, d1 = s ||x - c'_p1|| bounded from
-      // k1: d1^2 = S'_p1 + ||xs||^2 <= k1 (1 + rho) + r1 wE + B0 + ||xs||^2
-      // (2 B0 more: the float64 scores may order j before p1 where the fp32 ones do not)
-      const float X = xn * s;
-      const float r1 = sqrtf(sCn[p1]);
-      const float d1sq = k1 + rho * fabsf(k1) + wE * r1 * 1.0001f + 3.0f * B0 + X * X * 1.0001f +
-                         4.0f * U24 * (fabsf(k1) + X * X);
-      Dm = fminf(sRmax[p1], 2.0f * sqrtf(fmaxf(d1sq, 0.0f)) * 1.0001f);
-    }
-    const float thr2 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k2)) + wE * Dm;
-    const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k3)) + wE * Dm;
+    const float thr2 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k2));
+    const float thr3 = 2.0f * B0 + rho * (fabsf(k1) + fabsf(k3));
     uint32_t kind = 0;
     if (!(k2 - k1 > thr2)) kind = (same_chain || !(k3 - k1 > thr3)) ? 2u : 1u;
     float u1 = 0.0f;
@@ -2951,31 +2904,12 @@ __global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
     const bool refine = REF && __ballot(kind != 0u) != 0ull;
     if (refine) {
       kb = key_bounds(xn * s, *A.xabs * s, DP, rho, 1);
-      // pair screen, per key: |2 s c'_j . e| <= r wE for a centroid of scaled norm r
-      if constexpr (PAIR) kb.e1 += wE * 1.0001f;
       if (kind != 0u) {
         u1 = kb.upper(k1);
         if (u1 < kb.lower(k2))
           kind = 0u;
         else if (kind == 2u && !same_chain && kb.lower(k3) > u1)
           kind = 1u;
-      }
-    }
-    if constexpr (PAIR) {
-      // every other centroid is settled against p1 (kind 1): p2's exact
-      // distance from p1's neighbour list may settle the pair too
-      if (__ballot(kind == 1u) != 0ull && kind == 1u) {
-        const uint4* lp = reinterpret_cast<const uint4*>(sPair + p1 * KM_PAIR_M);
-        float D12 = Dm;
-#pragma unroll
-        for (int m = 0; m < KM_PAIR_M / 4; ++m) {
-          const uint4 e = lp[m];
-          D12 = ((e.x & 255u) == p2) ? __uint_as_float(e.x & ~255u) : D12;
-          D12 = ((e.y & 255u) == p2) ? __uint_as_float(e.y & ~255u) : D12;
-          D12 = ((e.z & 255u) == p2) ? __uint_as_float(e.z & ~255u) : D12;
-          D12 = ((e.w & 255u) == p2) ? __uint_as_float(e.w & ~255u) : D12;
-        }
-        if (k2 - k1 > 2.0f * B0 + rho * (fabsf(k1) + fabsf(k2)) + wE * D12) kind = 0u;
       }
     }
     // p1, p2 in one chain, every other chain's best separated from k1: the
@@ -2995,7 +2929,7 @@ __global__ __launch_bounds__(256, 1) void k_fused16(FusedArgs A) {
         if ((uint32_t)(8 + c) != cs) o = kmin(o, __uint_as_float(v2));
         if ((uint32_t)(12 + c) != cs) o = kmin(o, __uint_as_float(v3));
       }
-      const float thr3x = 2.0f * B0 + rho * (fabsf(k1) + fabsf(o)) + wE * Dm;
+      const float thr3x = 2.0f * B0 + rho * (fabsf(k1) + fabsf(o));
       if (kind == 2u && same_chain && (o - k1 > thr3x || (REF && kb.lower(o) > u1))) kind = 3u;
     }
     const int lab = (p1 < (uint32_t)A.k) ? (int)p1 : 0;
@@ -3139,55 +3073,6 @@ __global__ __launch_bounds__(256) void k_frag_images16(const _Float16* __restric
   CloF[id] = *reinterpret_cast<const uint4*>(Clo + src);
 }
 
-// Pair screen table (k_fused16<..., PAIR>), one workgroup per centroid i of
-// the kp <= 256: D_ij = s ||c'_i - c'_j|| over the real centroids j != i
-// (float64 from the fp32 centroids, rounded up), their maximum rmax[i], and
-// the KM_PAIR_M nearest as entries (D rounded up to a multiple of 256 ulps) | j;
-// missing entries repeat (rmax, i), which no p2 != i matches.
-__global__ __launch_bounds__(256) void k_pair_table(const float* __restrict__ C32, int k, int kp, int dp,
-                                                    const float* __restrict__ xabs, const float* __restrict__ cabs,
-                                                    uint32_t* __restrict__ pairs, const int* __restrict__ gate) {
-  if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
-  __shared__ float ci[256];
-  __shared__ float sD[256];
-  __shared__ float red[4];
-  const int i = blockIdx.x, j = threadIdx.x;
-  const float s = mfma_scale(*xabs, *cabs);
-  for (int f = j; f < dp; f += 256) ci[f] = C32[(size_t)i * dp + f];
-  __syncthreads();
-  const bool valid = i < k && j < k && j != i;
-  float D = 0.0f;
-  if (valid) {
-    double d2 = 0.0;
-    for (int f = 0; f < dp; ++f) {
-      const double v = (double)C32[(size_t)j * dp + f] - (double)ci[f];
-      d2 = fma(v, v, d2);
-    }
-    D = (float)(sqrt(d2) * (double)s * (1.0 + 1e-6));
-  }
-  sD[j] = valid ? D : INFINITY;
-  // radius: block maximum
-  float m = D;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((j & 63) == 0) red[j >> 6] = m;
-  __syncthreads();
-  const float rmax = (i < k) ? fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])) : INFINITY;
-  auto pack = [](float v, int idx) { return ((__float_as_uint(v) + 255u) & ~255u) | (uint32_t)idx; };
-  uint32_t* out = pairs + (size_t)i * KM_PAIR_M;
-  const int nreal = (i < k) ? k - 1 : 0;
-  if (j < KM_PAIR_M && j >= nreal) out[j] = pack(rmax, i);
-  if (valid) {
-    int rank = 0;
-    for (int t = 0; t < kp; ++t) {
-      const float v = sD[t];
-      rank += (v < D || (v == D && t < j)) ? 1 : 0;
-    }
-    if (rank < KM_PAIR_M) out[rank] = pack(D, j);
-  }
-  if (j == 0) reinterpret_cast<float*>(pairs + (size_t)kp * KM_PAIR_M)[i] = rmax;
-}
-
 // screening-bound constants: B0 = alpha * ||x|| + beta (see k_assign_mfma)
 __global__ void k_bound_consts(const float* __restrict__ cmax, const float* __restrict__ xabs,
                                const float* __restrict__ cabs, int dp, int shape16, float* __restrict__ bnd,
@@ -3266,23 +3151,12 @@ bool fused16_ok(const Geometry& g) {
   return on && fused_path_ok(g) && g.dp % 32 == 0;
 }
 
-bool pair_ok(const Geometry& g) {
-#if !KM_PAIR && !defined(KM_DIAG)
-  (void)g;
-  return false;  // not built (launch_fused's KM_PAIR_BRANCH)
-#endif
-  static const int on = diag_env("KM_PAIR", KM_PAIR);
-  return on && fused16_ok(g) && g.kp <= 256 &&
-         (size_t)g.kp * 4 + (size_t)(g.dp + 1) * g.kp * 8 + (size_t)g.kp * (KM_PAIR_M + 1) * 4 <= 160 * 1024;
-}
-size_t pair_words(const Geometry& g) { return pair_ok(g) ? (size_t)g.kp * (KM_PAIR_M + 1) : 0; }
-
 hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, const _Float16* Chi,
                         const _Float16* Clo, uint4* ChiF, uint4* CloF, const float* cn2s, const float* bnd,
                         const float* xabs, const float* cabs, int32_t* labels, QEntry* queue, uint32_t* qcount,
                         double* stats, int with_stats, int mode, int n_cu, QLayout* ql, const int* gate,
                         hipStream_t s, const float* C32, const float* cmax, float* bal, const double* C64P,
-                        double* sse, uint32_t* pairs) {
+                        double* sse) {
   ql->seg = 0;
   ql->nwaves = 0;
   if (g.n == 0) return hipSuccess;
@@ -3319,12 +3193,10 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
   }
 #endif
   const bool shape16 = fused16_ok(g);
-  const bool pair = pairs && pair_ok(g);
   if (shape16) {
     const int total = (g.kp / 16) * (g.dp / 32) * 64;
     hipLaunchKernelGGL(k_frag_images16, dim3((total + 255) / 256), dim3(256), 0, s, Chi, Clo, g.kp, g.dp, ChiF, CloF,
                        gate);
-    if (pair) hipLaunchKernelGGL(k_pair_table, dim3(g.kp), dim3(256), 0, s, C32, g.k, g.kp, g.dp, xabs, cabs, pairs, gate);
   } else {
     const int total = nb * ns * 64;
     hipLaunchKernelGGL(k_frag_images, dim3((total + 255) / 256), dim3(256), 0, s, Chi, Clo, g.kp, g.dp, ChiF, CloF, gate);
@@ -3339,9 +3211,8 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
   ql->seg = seg;
   ql->nwaves = (uint32_t)nw;
   FusedArgs a{X, xnorm, g.n, g.k, g.d, seg, ChiF, CloF, cn2s, bnd, xabs, cabs, labels, queue, qcount, stats, gate,
-                C64P, sse, pairs};
+                C64P, sse};
   const size_t lds = (size_t)g.kp * 4 + (with_stats ? (size_t)(g.dp + 1) * g.kp * 8 : 0);
-  [[maybe_unused]] const size_t lds_pair = (size_t)g.kp * (KM_PAIR_M + 1) * 4;
 #define KM_FUSED_CASE(NS_, NB_)                                                                        \
   case NS_ * 100 + NB_:                                                                                \
     if (with_stats && sse)                                                                             \
@@ -3355,7 +3226,6 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
     break;
 #define KM_FUSED16_CASE(NS2_, NB_)                                                                      \
   case NS2_ * 100 + NB_:                                                                                \
-    KM_PAIR_BRANCH(NS2_, NB_)                                                                           \
     if (with_stats && sse)                                                                              \
       KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, true, true, true>), dim3(nbk), dim3(256), lds, s, a);    \
     else if (with_stats && !refine)                                                                     \
@@ -3369,25 +3239,6 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
     else                                                                                                \
       KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, false>), dim3(nbk), dim3(256), lds, s, a);               \
     break;
-// the pair screen's instances (KP <= 256): built with -DKM_PAIR=1 and in the
-// diagnostic library (env KM_PAIR=1) only, since it lost end to end
-#if KM_PAIR || defined(KM_DIAG)
-#define KM_PAIR_BRANCH(NS2_, NB_)                                                                       \
-  if (pair && NB_ <= 8) {                                                                               \
-    KM_FUSED16_PAIR(NS2_, (NB_ <= 8 ? NB_ : 8))                                                         \
-  } else
-#else
-#define KM_PAIR_BRANCH(NS2_, NB_)
-#endif
-#define KM_FUSED16_PAIR(NS2_, NB_)                                                                      \
-  if (with_stats && sse)                                                                                \
-    KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, true, true, true, true>), dim3(nbk), dim3(256), lds + lds_pair, s, a);  \
-  else if (with_stats && !refine)                                                                       \
-    KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, true, false, false, true>), dim3(nbk), dim3(256), lds + lds_pair, s, a); \
-  else if (with_stats)                                                                                  \
-    KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, true, true, false, true>), dim3(nbk), dim3(256), lds + lds_pair, s, a);  \
-  else                                                                                                  \
-    KM_TIMED_LAUNCH((k_fused16<NS2_, NB_, false, true, false, true>), dim3(nbk), dim3(256), lds + lds_pair, s, a);
 #ifndef KM_F16_PREDICT
 #define KM_F16_PREDICT 0
 #endif
@@ -3404,8 +3255,6 @@ hipError_t launch_fused(const float* X, const float* xnorm, const Geometry& g, c
     return hipGetLastError();
   }
 #undef KM_FUSED16_CASE
-#undef KM_FUSED16_PAIR
-#undef KM_PAIR_BRANCH
   switch (ns * 100 + nb) {
     KM_FUSED_CASE(4, 2) KM_FUSED_CASE(4, 4) KM_FUSED_CASE(4, 6) KM_FUSED_CASE(4, 8)
     KM_FUSED_CASE(2, 2) KM_FUSED_CASE(2, 4) KM_FUSED_CASE(2, 6) KM_FUSED_CASE(2, 8) KM_FUSED_CASE(2, 12)

@@ -161,7 +161,6 @@ struct km_ctx {
   float* xnorm = nullptr;    // per-row upper bound of ||x|| (screening bound)
   uint4* ChiF = nullptr;     // fragment-linear hi / lo images (fused kernel)
   uint4* CloF = nullptr;
-  uint32_t* pairs = nullptr;  // pair screen neighbour table (km::pair_words)
   float* bnd = nullptr;      // screening-bound constants
   uint32_t* sort_scratch = nullptr;  // label sort of the large-k statistics
   size_t sort_words = 0;
@@ -282,7 +281,6 @@ void free_centroids(km_ctx* c) {
   dfree(c->cn2s);
   dfree(c->ChiF);
   dfree(c->CloF);
-  dfree(c->pairs);
   dfree(c->bnd);
   c->bal = nullptr;
   dfree(c->cmax);
@@ -617,7 +615,7 @@ int run_assign(km_ctx* c, bool with_stats) {
                               c->labels, c->queue, c->qcount, c->stats, with_stats ? 1 : 0,
                               (with_stats || c->screen >= km::KM_SCREEN_FAST1) ? c->screen : km::KM_SCREEN_X3_REFINE,
                               c->n_cu, &c->ql, c->gate, c->stream, c->C32, c->cmax, c->bal, c->C64P,
-                              sse ? sse_slot : nullptr, c->pairs));
+                              sse ? sse_slot : nullptr));
     }
     {
       // SSE: the fused kernel adds every decided row's residual, the
@@ -982,7 +980,6 @@ int km_set_centroids(km_ctx* c, const double* C, int32_t k, int32_t d) {
     KM_HIP(hipMalloc(&c->cn2s, sizeof(float) * kp));
     KM_HIP(hipMalloc(&c->ChiF, sizeof(_Float16) * kp * dp));
     KM_HIP(hipMalloc(&c->CloF, sizeof(_Float16) * kp * dp));
-    if (km::pair_words(c->g)) KM_HIP(hipMalloc(&c->pairs, sizeof(uint32_t) * km::pair_words(c->g)));
     KM_HIP(hipMalloc(&c->bnd, sizeof(float) * 16));
     c->bal = c->bnd + 4;  // [0, 1]: screening-bound constants; bal[0..10]: fast screen image maxima and bound constants
     KM_HIP(hipMalloc(&c->cmax, sizeof(float)));

@@ -49,9 +49,9 @@ def test_product_library_has_no_diagnostic_kernels():
     assert "k_fusedp" not in syms
     # the fast-screen experiment (k_fused1, k_prep_bal) is diagnostic-only too
     assert not re.search(r"k_fused1<", syms) and "k_prep_bal" not in syms
-    # and so is the two-MFMA pair screen (k_fused16's last template argument)
-    f16 = re.findall(r"k_fused16<\d+, \d+, (?:true|false), (?:true|false), (?:true|false), (true|false)>", syms)
-    assert f16 and set(f16) == {"false"}, set(f16)
+    # the two-MFMA pair screen is gone (round 6): k_fused16 has five template arguments
+    assert re.findall(r"k_fused16<\d+, \d+, (?:true|false), (?:true|false), (?:true|false)>", syms)
+    assert "k_pair_table" not in syms
     assert "getenv" not in subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True,
                                           text=True, check=True).stdout
 
