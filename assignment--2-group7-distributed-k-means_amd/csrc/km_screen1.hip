@@ -66,7 +66,10 @@ typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
 constexpr float U24 = 5.9604644775390625e-08f;  // 2^-24
 constexpr float U16 = 4.8828125e-04f;           // 2^-11, fp16 unit roundoff
-constexpr int S1_LMAX = 8;                      // candidates re-scored per row
+#ifndef KM_S1_LMAX  // A/B knob: 3, 4, 5 lost or tied (profiles/r6_c3_s1_lmax_ab.json)
+#define KM_S1_LMAX 8
+#endif
+constexpr int S1_LMAX = KM_S1_LMAX;             // candidates re-scored per row (more: the full scan)
 #ifndef KM_S1_NBUF
 #define KM_S1_NBUF 0  // register buffers of rows (tiles in flight + 1); 0: by row length
 #endif
