@@ -3948,7 +3948,7 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   if (e != hipSuccess) return e;
   const size_t tab_bytes = (size_t)(g.d + 1) * g.kp * 8;
   const size_t pres = (stats ? 2 : 1) * pre_bytes;
-  // (delta: direct atomics for the few rows that change clusters)
+  // (delta: the moves go to the change list, stats is null)
   const int tab_kp = (stats && !delta && tab_bytes + pres <= LDS_MAX) ? g.kp : 0;
   // workgroups of the re-rank, in percent of n_cu (KM_RERANK_PCT).  Each
   // flushes its [k][d+1] table with global atomics, but fewer workgroups lose

@@ -214,7 +214,7 @@ def _uneven_data(d, k):
 
 @pytest.mark.parametrize("d,k,delta", [
     (18, 1000, 1),   # dp 32, kp 1024: the LDS delta table fits for any grid on both ranks
-    (19, 1000, 1),   # fits only beside a small grid's wave prefix: direct atomics on both ranks
+    (19, 1000, 1),   # fits only beside a small grid's wave prefix: the fold's range count may differ by rank, the deltas do not
 ])
 def test_two_ranks_uneven_shards_same_statistics_mode(d, k, delta):
     import torch.multiprocessing as mp

@@ -344,15 +344,15 @@ def test_long_delta_fit_no_drift_vs_full_statistics():
 
 @pytest.mark.parametrize("n,d,k,centers", [
     (20000, 18, 1000, 300),   # dp 32, kp 1024 (unfused): k (d+1) 8 + the wave prefix fit LDS -> LDS aggregation
-    (20000, 19, 1000, 300),   # dp 32, kp 1024: 160,000 B of table + the prefix do not fit -> direct atomics
-    (20000, 60, 480, 200),    # dp 64, kp 512 (unfused): direct atomics
+    (20000, 19, 1000, 300),   # dp 32, kp 1024: 160,000 B of table + the prefix do not fit -> two cluster ranges
+    (20000, 60, 480, 200),    # dp 64, kp 512 (unfused): cluster ranges
 ])
 def test_unfused_geometries_delta_statistics(n, d, k, centers):
     # every k_s1 geometry takes delta statistics (round 6): k_s1_delta
     # aggregates the changed rows in an LDS [k][d+1] table where it fits
     # beside the largest grid's wave prefix (geometry and device only, never
-    # the rank's rows), else with direct float64 atomics; the resolvers move
-    # their changed rows with direct atomics
+    # the rank's rows), else over cluster ranges whose tables fit; the
+    # resolvers write their rows' moves into the same change list
     X = _blobs(n, d, centers, seed=21 + k + d)
     C0 = X[np.random.default_rng(22).choice(n, k, replace=False)]
     km = _check_fit(X, C0, 5)
@@ -422,7 +422,7 @@ def test_compute_sse_with_delta_statistics():
 
 @pytest.mark.parametrize("n,d,k,centers", [
     (12000, 64, 256, 64),     # c3 geometry: LDS delta table, fp32 table in LDS
-    (12000, 32, 1024, 256),   # c4 geometry: direct-atomic deltas, fp32 table in global memory
+    (12000, 32, 1024, 256),   # c4 geometry: deltas over two cluster ranges, fp32 table in global memory
 ])
 def test_tight_clusters_sse_delta_iterations(n, d, k, centers):
     # std 1e-3 in a +-1000 box (sum ||x||^2 ~ 1e12 x the SSE): the residuals to
@@ -452,7 +452,7 @@ def test_fit_c4_shape_labels_then_statistics_pass(compute_sse):
     # k = 1024, d = 32 (c4's geometry; BASELINE configs[3] has compute_sse on):
     # no fused statistics table fits, so the first iteration is k_s1's labels
     # and the statistics pass (with the SSE residuals); from the second on,
-    # delta statistics with direct float64 atomics (the [k][d+1] table does
+    # delta statistics folded over cluster ranges (the [k][d+1] table does
     # not fit LDS) and the residuals in k_s1: one read of X per iteration
     X = _blobs(30000, 32, 1024, seed=61)
     C0 = X[np.random.default_rng(62).choice(len(X), 1024, replace=False)]
@@ -509,7 +509,7 @@ def test_one_mfma_unfused_screen_fit_c5_shape():
 
 
 @pytest.mark.parametrize("n,d,k,centers,iters", [
-    (12000, 128, 4096, 1024, 4),  # c5 geometry: chunked images, one-MFMA screen, direct-atomic deltas
+    (12000, 128, 4096, 1024, 4),  # c5 geometry: chunked images, one-MFMA screen, deltas over 29 cluster ranges
     (12000, 64, 1536, 300, 5),    # dp 64, kp 1536 (no k_s1 instance): the same screen and deltas
 ])
 def test_one_mfma_unfused_screen_delta_statistics(n, d, k, centers, iters):
