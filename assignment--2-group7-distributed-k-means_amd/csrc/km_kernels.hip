@@ -3357,7 +3357,13 @@ __device__ __forceinline__ uint32_t find_segment(const uint32_t* __restrict__ pr
 // global float64 atomics.  The entries of all segments are spread over all
 // waves of the grid, 8 lanes per entry (np_pw8: lane u owns NumPy's
 // accumulator u, so the rounding is the reference's), 8 entries per wave.
-template <bool WIDE>  // WIDE: d > 256 (five pairwise halvings; 512 threads, 256 VGPRs)
+// PF (d <= 128, with the fp32 images C32 and their largest norm *cmax): the
+// candidates are first scored in fp32 (each lane its features u + 8 m, summed
+// over the 8 lanes) with k_fullscan's bounds [L, U] on ||x - c||; only those
+// whose L is at most the smallest U (x (1 + 8u)) are evaluated in float64,
+// and a single one is the answer without float64 (every other candidate is
+// farther by more than 4.8e-7 relative, far beyond NumPy's rounding)
+template <bool WIDE, bool PF = false>  // WIDE: d > 256 (five pairwise halvings; 512 threads, 256 VGPRs)
 __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __restrict__ X, int dp, int d, int k,
                                                   const double* __restrict__ C64, const QEntry* __restrict__ queue,
                                                   const uint32_t* __restrict__ qcount, QLayout ql,
@@ -3365,9 +3371,11 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
                                                   int tab_kp, double* __restrict__ sse, const int* __restrict__ gate,
                                                   const uint32_t* __restrict__ cand, uint32_t cand_cap, int delta,
                                                   const float* __restrict__ sse_c32, uint2* __restrict__ chg,
-                                                  const uint32_t* __restrict__ chg_cnt) {
+                                                  const uint32_t* __restrict__ chg_cnt,
+                                                  const float* __restrict__ C32, const float* __restrict__ cmax) {
   if (*gate) return;  // a stopped batch (km_update_async): the rest of it is a no-op
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const float cmv = PF ? *cmax : 0.0f;
   double* tab = reinterpret_cast<double*>(smem);
   uint32_t* pre = reinterpret_cast<uint32_t*>(smem + (stats && tab_kp ? (size_t)(d + 1) * tab_kp * 8 : 0));
   uint32_t* pre1 = pre + ql.nwaves + 1;  // full / chain scan entries (their sums only)
@@ -3401,8 +3409,61 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
     double mnorm = 0.0;  // the chosen centroid's norm (SSE)
     // np.argmin over ascending candidates, two norms per pass (NumPy's
     // pairwise order, 8 lanes per entry); kind 1 is the pass over {i1, i2}
-    const int npass = rec ? (ok ? (nc + 1) / 2 : 0) : 1;
+    int npass = rec ? (ok ? (nc + 1) / 2 : 0) : 1;
     int bi = -1;
+    const int ncand = rec ? nc : 2;
+    uint32_t keep = 0xFFFFu;  // candidate positions evaluated in float64
+    if constexpr (PF) {
+      // fp32 prefilter (see above); positions p < ncand, ascending indices
+      bool fin = ok;
+      float xr[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int f = u + 8 * m;
+        xr[m] = (ok && f < d) ? x[f] : 0.0f;
+        fin = fin && fabsf(xr[m]) <= 3.0e38f;
+      }
+      fin = fin && (cmv <= 3.0e38f);
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) fin = fin && __shfl_xor((int)fin, o) != 0;
+      if (fin) {
+        const float e = ((float)((d + 7) / 8 + 8) * 0.5f + 8.0f) * U24 * 1.1f;
+        const float gam = U24 * cmv * 1.01f + 1e-37f;
+        float Lp[CAND_REC - 1];
+        float Us = FLT_MAX;
+#pragma unroll
+        for (int p = 0; p < CAND_REC - 1; ++p) {
+          Lp[p] = FLT_MAX;
+          if (p < ncand) {
+            const int j = rec ? (int)rec[1 + p] : (p == 0 ? (int)min(q.i1, q.i2) : (int)max(q.i1, q.i2));
+            const float* cj = C32 + (size_t)j * dp;
+            float D = 0.0f;
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+              const int f = u + 8 * m;
+              const float df = xr[m] - (f < d ? cj[f] : 0.0f);
+              D = fmaf(df, df, D);
+            }
+#pragma unroll
+            for (int o = 1; o < 8; o <<= 1) D += __shfl_xor(D, o);
+            const bool tiny = !(D >= 0x1p-96f);
+            const float r = __builtin_amdgcn_sqrtf(tiny ? 0x1p-96f : D);
+            const float U = fmaf(r, 1.0f + e, gam) * (1.0f + 4.0f * U24);
+            Lp[p] = fmaf(tiny ? 0.0f : r, 1.0f - e, -gam) * (1.0f - 4.0f * U24);
+            Us = fminf(Us, U);
+          }
+        }
+        keep = 0u;
+#pragma unroll
+        for (int p = 0; p < CAND_REC - 1; ++p) keep |= (Lp[p] <= Us * (1.0f + 8.0f * U24)) ? (1u << p) : 0u;
+        if (__popc(keep) == 1 && !(sse && !sse_c32)) {
+          // one candidate left: NumPy's argmin (no float64 needed)
+          const int p1 = __ffs(keep) - 1;
+          bi = rec ? (int)rec[1 + p1] : (p1 == 0 ? (int)min(q.i1, q.i2) : (int)max(q.i1, q.i2));
+          npass = 0;
+        }
+      }
+    }
     for (int t = 0; t < npass; ++t) {
       int a, bb;
       if (rec) {
@@ -3411,6 +3472,14 @@ __global__ __launch_bounds__(WIDE ? 512 : 1024) void k_rerank2(const float* __re
       } else {
         a = ok ? (int)min(q.i1, q.i2) : 0;
         bb = ok ? (int)max(q.i1, q.i2) : 0;
+      }
+      if constexpr (PF) {
+        // positions dropped by the prefilter: skipped (a pair with one kept
+        // evaluates it twice, as the odd tail does)
+        const bool ka = (keep >> (2 * t)) & 1u, kb = 2 * t + 1 < ncand && ((keep >> (2 * t + 1)) & 1u);
+        if (!ka && !kb) continue;
+        if (!ka) a = bb;
+        if (!kb) bb = a;
       }
       const double* __restrict__ ca = C64 + (size_t)a * d;
       const double* __restrict__ cb = C64 + (size_t)bb * d;
@@ -3956,14 +4025,20 @@ hipError_t launch_resolve(const float* X, const Geometry& g, const double* C64, 
   // 0.48 at 50%, 0.80 at 25%)
   static const int rpct = diag_env("KM_RERANK_PCT", KM_RERANK_PCT);
   const int rwg = std::max(1, n_cu * std::max(1, rpct) / 100);
+  // the re-rank's fp32 prefilter (KM_RR_PF, default on) where rows are <= 128 wide
+  static const int rr_pf = diag_env("KM_RR_PF", 1);
   if (g.d > 256)
     hipLaunchKernelGGL(k_rerank2<true>, dim3(rwg), dim3(512), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
                        g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap, delta, sse_c32, chg,
-                       chg_cnt);
+                       chg_cnt, C32, cmax);
+  else if (rr_pf && g.d <= 128 && C32 && cmax)
+    hipLaunchKernelGGL((k_rerank2<false, true>), dim3(rwg), dim3(1024), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp,
+                       g.d, g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap, delta, sse_c32,
+                       chg, chg_cnt, C32, cmax);
   else
     hipLaunchKernelGGL(k_rerank2<false>, dim3(rwg), dim3(1024), (tab_kp ? tab_bytes : 0) + pres, s, X, g.dp, g.d,
                        g.k, C64, queue, qcount, ql, labels, stats, tab_kp, sse, gate, cand, cand_cap, delta, sse_c32, chg,
-                       chg_cnt);
+                       chg_cnt, C32, cmax);
   return hipGetLastError();
 }
 
