@@ -571,3 +571,28 @@ def test_full_scan_prefilter_equidistant_groups(d, k, group):
     C[ng * group] = C[0]  # an exact duplicate: the lower index wins
     a, eng = _predict(X, C)
     np.testing.assert_array_equal(a, orc.assign(X, C)[0])
+
+
+@pytest.mark.parametrize("d,k", [(128, 4096), (64, 1536), (64, 256)])
+def test_rerank_prefilter_relative_gaps(d, k):
+    # rows whose two nearest centroids differ in distance by a relative gap
+    # around the fp32 prefilter's margin (8u = 4.8e-7 and its bounds' e):
+    # below it both stay for float64, above it one is kept and decides alone;
+    # labels must be the oracle's on both sides (and for exact ties)
+    rng = np.random.default_rng(d + k + 7)
+    nrow = 4000
+    X = rng.uniform(-5, 5, (nrow, d)).astype(np.float32).astype(np.float64)
+    C = rng.uniform(-5, 5, (k, d)) * 3.0
+    gaps = [0.0, 1e-9, 1e-7, 3e-7, 1e-6, 3e-6, 1e-5, 1e-4]
+    npairs = min(nrow, k // 2)
+    for i in range(npairs):
+        u = rng.standard_normal((2, d))
+        u /= np.linalg.norm(u, axis=1, keepdims=True)
+        r = 0.7
+        gap = gaps[i % len(gaps)]
+        C[2 * i] = X[i] + r * u[0]
+        C[2 * i + 1] = X[i] + r * (1.0 + gap) * u[1]
+        if i % 2:
+            C[[2 * i, 2 * i + 1]] = C[[2 * i + 1, 2 * i]]  # the nearer one at the higher index half the time
+    a, eng = _predict(X, C)
+    np.testing.assert_array_equal(a, orc.assign(X, C)[0])
