@@ -1,0 +1,12 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+OUT=gpurun_out/r6_c2_r5ab; mkdir -p $OUT
+for R in 1 2 3; do
+  (cd gpurun_ab_r5 && timeout -k 10 300 python -u bench.py --config c2 --no-cpu-baseline > ../$OUT/r5.$R.json 2> ../$OUT/r5.$R.err) || { echo r5 failed; tail -5 $OUT/r5.$R.err; exit 1; }
+  timeout -k 10 300 python -u bench.py --config c2 --no-cpu-baseline --no-first-iter > $OUT/r6.$R.json 2> $OUT/r6.$R.err || { echo r6 failed; tail -5 $OUT/r6.$R.err; exit 1; }
+  python3 -c "
+import json
+for t in ['r5','r6']:
+    d=json.loads(open('$OUT/'+t+'.$R.json').read().strip().splitlines()[-1]); print(t, $R, round(d['value'],1), d['kernel_avg_ms'])"
+done
