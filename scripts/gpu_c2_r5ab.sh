@@ -1,3 +1,7 @@
+# c2 on one box, alternating: the round-5 library and package against the
+# current one (profiles/r6_c2_r5_ab.json).  gpurun_ab_r5/ is staged before the
+# call from commit 19c48c3 (git worktree add; make in its csrc; copy the
+# package, bench.py, kmeans_amd.py and oracle/) and deleted afterwards.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
