@@ -1021,41 +1021,57 @@ __global__ __launch_bounds__(1024) void k_s1_delta(const float* __restrict__ X, 
                                                    int nr, double* __restrict__ stats,
                                                    const int* __restrict__ gate) {
   if (*gate) return;
-  extern __shared__ double smem_d[];  // [kr][d + 1], then pre[nw + 1]
+  extern __shared__ double smem_d[];  // [kr][d + 1], then pre[nw + 1] and 16 wave sums
   const int d1 = d + 1;
   double* tab = smem_d;
   uint32_t* pre = reinterpret_cast<uint32_t*>(smem_d + (size_t)kr * d1);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-  if (wave == 0) {
-    uint32_t run = 0;
-    for (int b = 0; b < nw; b += 64) {
-      uint32_t v = 0;
-      if (b + lane < nw) {
-        v = cnt[b + lane];
-        if (qcount) v += qcount[2 * (b + lane)] + qcount[2 * (b + lane) + 1];
-        v = min(v, seg);
-      }
-      uint32_t inc = v;
+  {
+    // exclusive prefix of the segment totals over the whole workgroup: thread
+    // t owns segments [t c, (t + 1) c), a wave scan, then the waves' sums
+    // (one pass of independent loads instead of a dependent loop on wave 0)
+    uint32_t* wsum = pre + nw + 1;  // [16]
+    auto total = [&](int w) {
+      uint32_t v = cnt[w];
+      if (qcount) v += qcount[2 * w] + qcount[2 * w + 1];
+      return min(v, seg);
+    };
+    const int nt = (int)blockDim.x, t = (int)threadIdx.x;
+    const int c = (nw + nt - 1) / nt, b0 = t * c;
+    uint32_t v = 0;
+    for (int i = 0; i < c; ++i)
+      if (b0 + i < nw) v += total(b0 + i);
+    uint32_t inc = v;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(inc, o);
-        inc += lane >= o ? t : 0u;
-      }
-      if (b + lane < nw) pre[b + lane] = run + inc - v;
-      run += __shfl(inc, 63);
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o);
+      inc += lane >= o ? u : 0u;
     }
-    if (lane == 0) pre[nw] = run;
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int i = 0; i < wave; ++i) base += wsum[i];
+    uint32_t run = base + inc - v;
+    for (int i = 0; i < c; ++i)
+      if (b0 + i < nw) {
+        pre[b0 + i] = run;
+        run += total(b0 + i);
+      }
+    if (t == nt - 1) pre[nw] = run;
   }
   __syncthreads();
   const int r = (int)(blockIdx.x % (uint32_t)nr);
   const uint32_t ns = gridDim.x / (uint32_t)nr, sl = blockIdx.x / (uint32_t)nr;
   const uint32_t nc = pre[nw];
-  const uint32_t per = max(S1D_MIN, (nc + ns - 1u) / ns);
+  // a slice is at least S1D_MIN entries and 1/16 of the table: every busy
+  // workgroup flushes its whole table with global atomics, so a short list
+  // spread over all workgroups would contend on the same addresses
+  const uint32_t lo = (uint32_t)r * (uint32_t)kr;
+  const uint32_t span = min((uint32_t)kr, (uint32_t)k - lo);
+  const uint32_t per = max(max(S1D_MIN, (uint32_t)kr * (uint32_t)d1 / 16u), (nc + ns - 1u) / ns);
   const uint32_t e0 = sl * per;
   if (sl >= ns || e0 >= nc) return;
   const uint32_t e1 = min(nc, e0 + per);
-  const uint32_t lo = (uint32_t)r * (uint32_t)kr;
-  const uint32_t span = min((uint32_t)kr, (uint32_t)k - lo);
   for (int i = threadIdx.x; i < (int)span * d1; i += blockDim.x) tab[i] = 0.0;
   __syncthreads();
   // entry e of the concatenation: segment w = the last with pre[w] <= e; a
@@ -1168,7 +1184,7 @@ hipError_t launch_chg_delta(const float* X, const Geometry& g, const uint2* chg,
   if (g.n == 0 || nw == 0) return hipSuccess;
   if (g.k > 65535) return hipErrorInvalidValue;
   constexpr size_t LDS = 160 * 1024;
-  const size_t pre = ((size_t)nw + 1) * 4;
+  const size_t pre = ((size_t)nw + 1 + 16) * 4;  // + the prefix's per-wave sums
   const size_t row = (size_t)(g.d + 1) * 8;  // one cluster's table row
   if (pre > 64 * 1024 || pre + row > LDS) return hipErrorInvalidValue;
   // ranges of clusters whose [kr][d+1] table fits beside the prefix, as few
